@@ -1,0 +1,113 @@
+"""ctypes mirror of include/crdtgpu.h and the loader of libcrdtgpu.so.
+
+The library is the product: there is no fallback.  If it is missing or fails
+to load, importing this module raises -- a GPU box must never silently run a
+CPU path.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+import re
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libcrdtgpu.so")
+HEADER_PATH = os.path.join(os.path.dirname(os.path.dirname(HERE)), "include", "crdtgpu.h")
+
+CRDT_OK = 0
+CRDT_E_INVALID = -1
+CRDT_E_ACTOR_RANGE = -2
+CRDT_E_UNSORTED = -3
+CRDT_E_CAPACITY = -4
+CRDT_E_HIP = -5
+CRDT_E_NOMEM = -6
+CRDT_E_WORKSPACE = -7
+CRDT_MAX_R = 64
+CRDT_FOLD_AWSET = 0
+CRDT_FOLD_DELTA = 1
+
+_vp = ctypes.c_void_p
+_u32 = ctypes.c_uint32
+_u64 = ctypes.c_uint64
+
+
+class CAWSetBatch(ctypes.Structure):
+    _fields_ = [
+        ("n_docs", _u32), ("R", _u32),
+        ("offsets", _vp), ("counts", _vp), ("keys", _vp), ("actors", _vp), ("counters", _vp), ("vv", _vp),
+    ]
+
+
+class CAWSetOut(ctypes.Structure):
+    _fields_ = [("offsets", _vp), ("counts", _vp), ("keys", _vp), ("actors", _vp), ("counters", _vp), ("vv", _vp)]
+
+
+class CSrcBatch(ctypes.Structure):
+    _fields_ = [
+        ("n_docs", _u32), ("R", _u32),
+        ("doc_srcs", _vp), ("src_actor", _vp), ("vv", _vp), ("entry_off", _vp),
+        ("keys", _vp), ("actors", _vp), ("counters", _vp),
+        ("tomb_off", _vp), ("tkeys", _vp), ("tactors", _vp), ("tcounters", _vp),
+    ]
+
+
+class CrdtError(RuntimeError):
+    def __init__(self, code: int, what: str = ""):
+        self.code = code
+        msg = "%s (code %d)" % (strerror(code) if _lib is not None else "crdtgpu error", code)
+        super().__init__(what + ": " + msg if what else msg)
+
+
+def header_functions(path: str = HEADER_PATH):
+    """Names of the functions include/crdtgpu.h declares."""
+    text = open(path).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"^\s*(?:int|void|const char\*)\s+(crdt_\w+)\s*\(", text, flags=re.M)))
+
+
+def _load():
+    if not os.path.exists(LIB_PATH):
+        raise ImportError("libcrdtgpu.so not built at %s: run `python -c 'import __graft_entry__ as g; g.build()'`"
+                          % LIB_PATH)
+    lib = ctypes.CDLL(LIB_PATH)
+    P = ctypes.POINTER
+    sig = {
+        "crdt_abi_version": (ctypes.c_int, []),
+        "crdt_strerror": (ctypes.c_char_p, [ctypes.c_int]),
+        "crdt_ctx_create": (ctypes.c_int, [ctypes.c_int, P(_vp)]),
+        "crdt_ctx_destroy": (None, [_vp]),
+        "crdt_ctx_reserve": (ctypes.c_int, [_vp, _u32, _u64]),
+        "crdt_ctx_sync": (ctypes.c_int, [_vp, _vp]),
+        "crdt_awset_join_async": (ctypes.c_int, [_vp, P(CAWSetBatch), P(CAWSetBatch), P(CAWSetOut), _vp]),
+        "crdt_awset_fold_async": (ctypes.c_int, [_vp, ctypes.c_int, P(CAWSetBatch), P(CSrcBatch), P(CAWSetOut), _vp]),
+        "crdt_vv_max_async": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_size_t, _vp]),
+        "crdt_causal_context_async": (ctypes.c_int, [_vp, _vp, _u32, _u32, _vp, _vp]),
+        "crdt_gen_pair_async": (ctypes.c_int, [_vp, _u64, _u32, P(CAWSetOut), P(CAWSetOut), _vp]),
+        "crdt_awset_join_batch": (ctypes.c_int, [_vp, P(CAWSetBatch), P(CAWSetBatch), P(CAWSetOut)]),
+        "crdt_awset_fold_batch": (ctypes.c_int, [_vp, ctypes.c_int, P(CAWSetBatch), P(CSrcBatch), P(CAWSetOut)]),
+        "crdt_validate_batch": (ctypes.c_int, [P(CAWSetBatch)]),
+        "crdt_validate_src_batch": (ctypes.c_int, [P(CSrcBatch)]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(lib, name)
+        f.restype = res
+        f.argtypes = args
+    return lib
+
+
+_lib = None
+_lib = _load()
+
+
+def lib():
+    return _lib
+
+
+def strerror(code: int) -> str:
+    return _lib.crdt_strerror(code).decode()
+
+
+def check(code: int, what: str = "") -> None:
+    if code != CRDT_OK:
+        raise CrdtError(code, what)

@@ -1,0 +1,248 @@
+"""Host mirror of the reference's Go API, merging on the GPU.
+
+Same types and method names as package crdt:
+  Dot, VersionVector           crdt-misc.go:9-74
+  AWSet                        awset.go:55-171
+  AWSetDelta                   awset-delta_test.go:9-77
+plus the batch entry points a caller with many documents uses:
+  MergeBatch(dsts, srcs)                 one (*AWSet).Merge per pair
+  FoldBatch(dsts, srcs_per_dst)          ordered (*AWSet).Merge sequences
+  DeltaMergeBatch(dsts, srcs_per_dst)    ordered (*AWSetDelta).Merge sequences
+
+``Merge`` / ``*Batch`` intern the string keys of the batch into u64 ids
+(order-preserving, an exact bijection), pack structure-of-arrays buffers, run
+the join/fold kernels through ``crdt_awset_join_batch`` /
+``crdt_awset_fold_batch`` and unpack the result into the Go-shaped maps.  The
+local ops (Add, Del, Clone, ...) are per-replica host state changes, as in the
+reference; they are not part of the batched hot path.
+
+Differences from the Go code, all at inputs where Go panics or is ambiguous:
+  * a batch's version vectors are zero-padded to the longest one (R <= 64);
+    ``HasDot`` at actor == len(vv) of a shorter vector then reads the pad
+    instead of panicking.  Equal-length vectors (every reference test) are exact.
+  * where Go panics (actor == len(vv)), the merge raises CrdtError
+    (CRDT_E_ACTOR_RANGE) and leaves the destination untouched.
+"""
+
+from __future__ import annotations
+
+from typing import Dict, List, NamedTuple, Optional, Sequence
+
+from . import abi
+from .batch import AWSetBatch, SrcBatch
+from .engine import Engine
+
+
+class Dot(NamedTuple):
+    """crdt-misc.go:12-15."""
+
+    Actor: int
+    Counter: int
+
+    def String(self) -> str:  # crdt-misc.go:17-19
+        return "(%s %d)" % (chr(ord("A") + self.Actor), self.Counter)
+
+    __str__ = String
+
+
+class VersionVector(list):
+    """crdt-misc.go:23; single-vector host helpers (the batched max runs in the kernels)."""
+
+    def HasDot(self, d: Dot) -> bool:  # crdt-misc.go:28-34
+        if len(self) < d.Actor:
+            return False
+        if d.Actor == len(self):
+            raise abi.CrdtError(abi.CRDT_E_ACTOR_RANGE, "HasDot")
+        return self[d.Actor] >= d.Counter
+
+    def Counter(self, a: int) -> int:  # crdt-misc.go:36-41
+        if len(self) < a:
+            return 0
+        if a == len(self):
+            raise abi.CrdtError(abi.CRDT_E_ACTOR_RANGE, "Counter")
+        return self[a]
+
+    def Merge(self, src: Sequence[int]) -> None:  # crdt-misc.go:43-55
+        for i, n in enumerate(src):
+            if i < len(self):
+                if self[i] < n:
+                    self[i] = n
+            else:
+                self.append(n)
+
+    def Clone(self) -> "VersionVector":  # crdt-misc.go:70-74
+        return VersionVector(self)
+
+    def String(self) -> str:  # crdt-misc.go:57-68
+        return "[" + ", ".join("(%s %d)" % (chr(ord("A") + i), n) for i, n in enumerate(self)) + "]"
+
+    __str__ = String
+
+
+_engine: Optional[Engine] = None
+
+
+def default_engine() -> Engine:
+    global _engine
+    if _engine is None:
+        _engine = Engine(0)
+    return _engine
+
+
+class AWSet:
+    """awset.go:55-59."""
+
+    def __init__(self, Actor: int = 0, VersionVector_: Optional[Sequence[int]] = None,
+                 Entries: Optional[Dict[str, Dot]] = None):
+        self.Actor = Actor
+        self.VersionVector = VersionVector(VersionVector_ or [])
+        self.Entries: Dict[str, Dot] = dict(Entries or {})
+
+    def SortedValues(self) -> List[str]:  # awset.go:61-70
+        return sorted(self.Entries)
+
+    def Reset(self) -> None:  # awset.go:72-75
+        self.VersionVector = VersionVector([0])
+        self.Entries = {}
+
+    def Clone(self) -> "AWSet":  # awset.go:77-85
+        return AWSet(self.Actor, list(self.VersionVector), self.Entries)
+
+    def Has(self, k: str) -> bool:  # awset.go:87
+        return k in self.Entries
+
+    def Add(self, *keys: str) -> None:  # awset.go:89-94
+        for k in keys:
+            if self.Actor >= len(self.VersionVector):
+                raise abi.CrdtError(abi.CRDT_E_ACTOR_RANGE, "Add")
+            self.VersionVector[self.Actor] += 1
+            self.Entries[k] = Dot(self.Actor, self.VersionVector[self.Actor])
+
+    def Del(self, *keys: str) -> None:  # awset.go:96-101 (no clock bump)
+        for k in keys:
+            self.Entries.pop(k, None)
+
+    def Merge(self, src: "AWSet") -> None:  # awset.go:103-105, on the GPU
+        MergeBatch([self], [src])
+
+    def String(self) -> str:  # awset.go:163-171
+        s = self.VersionVector.String()
+        for v in self.SortedValues():
+            s += '\n  %s  "%s"' % (self.Entries[v], v)
+        return s
+
+    __str__ = String
+
+
+class AWSetDelta(AWSet):
+    """awset-delta_test.go:9-12."""
+
+    def __init__(self, Actor: int = 0, VersionVector_: Optional[Sequence[int]] = None,
+                 Entries: Optional[Dict[str, Dot]] = None, Deleted: Optional[Dict[str, Dot]] = None):
+        super().__init__(Actor, VersionVector_, Entries)
+        self.Deleted: Optional[Dict[str, Dot]] = dict(Deleted) if Deleted else None
+
+    def Del(self, *keys: str) -> None:  # awset-delta_test.go:14-33
+        if self.Actor >= len(self.VersionVector):
+            raise abi.CrdtError(abi.CRDT_E_ACTOR_RANGE, "Del")
+        self.VersionVector[self.Actor] += 1
+        dot2 = Dot(self.Actor, self.VersionVector[self.Actor])
+        for k in keys:
+            if k in self.Entries:
+                if self.Deleted is None:
+                    self.Deleted = {}
+                self.Deleted[k] = dot2
+                del self.Entries[k]
+
+    def Clone(self) -> "AWSetDelta":  # awset-delta_test.go:35-49
+        return AWSetDelta(self.Actor, list(self.VersionVector), self.Entries, self.Deleted)
+
+    def Merge(self, src: "AWSetDelta") -> None:  # awset-delta_test.go:51-65, on the GPU
+        DeltaMergeBatch([self], [[src]])
+
+    def gcDeleted(self, srcVersionVector) -> None:  # awset-delta_test.go:67-77: empty in the reference
+        pass
+
+
+# ---------------------------------------------------------------------------
+# packing
+
+
+def _intern(states) -> Dict[str, int]:
+    keys = set()
+    for s in states:
+        keys.update(s.Entries)
+        if isinstance(s, AWSetDelta) and s.Deleted:
+            keys.update(s.Deleted)
+    return {k: i for i, k in enumerate(sorted(keys))}
+
+
+def _entries(m: Optional[Dict[str, Dot]], ids) -> list:
+    return sorted((ids[k], d.Actor, d.Counter) for k, d in (m or {}).items())
+
+
+def _pad(vv, R):
+    return list(vv) + [0] * (R - len(vv))
+
+
+def _width(states) -> int:
+    R = max([len(s.VersionVector) for s in states] + [1])
+    if R > abi.CRDT_MAX_R:
+        raise abi.CrdtError(abi.CRDT_E_INVALID, "version vector longer than %d" % abi.CRDT_MAX_R)
+    return R
+
+
+def _unpack(dsts, out, names, R, widths):
+    for d, dst in enumerate(dsts):
+        o, n = int(out.offsets[d]), int(out.counts[d])
+        keys = out.keys[o:o + n].tolist()
+        acts = out.actors[o:o + n].tolist()
+        cnts = out.counters[o:o + n].tolist()
+        dst.Entries = {names[k]: Dot(a, c) for k, a, c in zip(keys, acts, cnts)}
+        dst.VersionVector = VersionVector(out.vv[d * R:d * R + widths[d]].tolist())
+
+
+def MergeBatch(dsts: Sequence[AWSet], srcs: Sequence[AWSet], engine: Optional[Engine] = None) -> None:
+    """dsts[i].Merge(srcs[i]) for every i, as one batched GPU join (dsts must be distinct)."""
+    if len(dsts) != len(srcs):
+        raise ValueError("MergeBatch: length mismatch")
+    if not dsts:
+        return
+    states = list(dsts) + list(srcs)
+    ids = _intern(states)
+    names = {i: k for k, i in ids.items()}
+    R = _width(states)
+    db = AWSetBatch.from_docs(R, [(_entries(s.Entries, ids), _pad(s.VersionVector, R)) for s in dsts])
+    sb = AWSetBatch.from_docs(R, [(_entries(s.Entries, ids), _pad(s.VersionVector, R)) for s in srcs])
+    out = (engine or default_engine()).join(db, sb)
+    widths = [max(len(a.VersionVector), len(b.VersionVector)) for a, b in zip(dsts, srcs)]
+    _unpack(dsts, out, names, R, widths)
+
+
+def _fold(mode, dsts, srcs_per_dst, engine):
+    if len(dsts) != len(srcs_per_dst):
+        raise ValueError("length mismatch")
+    if not dsts:
+        return
+    states = list(dsts) + [s for lst in srcs_per_dst for s in lst]
+    ids = _intern(states)
+    names = {i: k for k, i in ids.items()}
+    R = _width(states)
+    db = AWSetBatch.from_docs(R, [(_entries(s.Entries, ids), _pad(s.VersionVector, R)) for s in dsts])
+    per_doc = [[(s.Actor, _pad(s.VersionVector, R), _entries(s.Entries, ids),
+                 _entries(getattr(s, "Deleted", None), ids)) for s in lst] for lst in srcs_per_dst]
+    sb = SrcBatch.from_lists(R, per_doc)
+    out = (engine or default_engine()).fold(mode, db, sb)
+    widths = [max([len(d.VersionVector)] + [len(s.VersionVector) for s in lst]) for d, lst in zip(dsts, srcs_per_dst)]
+    _unpack(dsts, out, names, R, widths)
+
+
+def FoldBatch(dsts: Sequence[AWSet], srcs_per_dst: Sequence[Sequence[AWSet]], engine: Optional[Engine] = None):
+    """for each i, for src in srcs_per_dst[i] in order: dsts[i].Merge(src)."""
+    _fold(abi.CRDT_FOLD_AWSET, dsts, srcs_per_dst, engine)
+
+
+def DeltaMergeBatch(dsts: Sequence[AWSetDelta], srcs_per_dst: Sequence[Sequence[AWSetDelta]],
+                    engine: Optional[Engine] = None):
+    """for each i, for src in srcs_per_dst[i] in order: dsts[i].Merge(src) (AWSetDelta semantics)."""
+    _fold(abi.CRDT_FOLD_DELTA, dsts, srcs_per_dst, engine)

@@ -1,0 +1,217 @@
+"""SoA batch containers matching include/crdtgpu.h.
+
+A batch's arrays are either numpy arrays (host: the synchronous ``*_batch``
+entry points) or torch tensors on a HIP device (the ``*_async`` entry points,
+inputs resident in HBM).  Device tensors use torch.int32 / torch.int64, whose
+bits are the ABI's u32 / u64.
+"""
+
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from .abi import CAWSetBatch, CAWSetOut, CSrcBatch
+
+U32, U64 = np.uint32, np.uint64
+
+
+def _is_torch(a) -> bool:
+    return a is not None and type(a).__module__.startswith("torch")
+
+
+def ptr(a):
+    if a is None:
+        return None
+    if isinstance(a, np.ndarray):
+        if not a.flags.c_contiguous:
+            raise ValueError("array must be C-contiguous")
+        return a.ctypes.data
+    if not a.is_contiguous():
+        raise ValueError("tensor must be contiguous")
+    return a.data_ptr()
+
+
+def _np(a, dtype):
+    if a is None:
+        return None
+    if _is_torch(a):
+        a = a.detach().cpu().numpy()
+    return np.ascontiguousarray(a).view(dtype) if a.dtype.itemsize == np.dtype(dtype).itemsize else \
+        np.ascontiguousarray(a, dtype=dtype)
+
+
+def _torch(a, device):
+    import torch
+
+    if a is None:
+        return None
+    if _is_torch(a):
+        return a.to(device)
+    sdt = {4: (np.int32, torch.int32), 8: (np.int64, torch.int64)}[a.dtype.itemsize]
+    return torch.from_numpy(np.ascontiguousarray(a).view(sdt[0])).to(device)
+
+
+class AWSetBatch:
+    """n_docs AWSet states: doc d owns slots [offsets[d], offsets[d+1]), live = counts[d]."""
+
+    def __init__(self, R, offsets, keys, actors, counters, vv, counts=None):
+        self.R = int(R)
+        self.offsets, self.keys, self.actors, self.counters, self.vv, self.counts = (
+            offsets, keys, actors, counters, vv, counts)
+
+    @property
+    def n_docs(self) -> int:
+        return int(self.offsets.shape[0]) - 1
+
+    def c(self) -> CAWSetBatch:
+        return CAWSetBatch(self.n_docs, self.R, ptr(self.offsets), ptr(self.counts), ptr(self.keys),
+                           ptr(self.actors), ptr(self.counters), ptr(self.vv))
+
+    def numpy(self) -> "AWSetBatch":
+        return AWSetBatch(self.R, _np(self.offsets, U32), _np(self.keys, U64), _np(self.actors, U32),
+                          _np(self.counters, U64), _np(self.vv, U64), _np(self.counts, U32))
+
+    def to(self, device) -> "AWSetBatch":
+        return AWSetBatch(self.R, *(_torch(a, device) for a in (self.offsets, self.keys, self.actors,
+                                                                  self.counters, self.vv)),
+                          counts=_torch(self.counts, device))
+
+    # -- host helpers ---------------------------------------------------
+    @staticmethod
+    def from_docs(R, docs, slack=0) -> "AWSetBatch":
+        """docs: list of (entries [(key, actor, counter)] sorted by key, vv [R])."""
+        n = len(docs)
+        counts = np.array([len(e) for e, _ in docs], dtype=U32)
+        caps = counts + U32(slack)
+        offsets = np.zeros(n + 1, dtype=U32)
+        np.cumsum(caps, out=offsets[1:])
+        total = int(offsets[-1])
+        keys = np.zeros(total, dtype=U64)
+        actors = np.zeros(total, dtype=U32)
+        counters = np.zeros(total, dtype=U64)
+        vv = np.zeros(n * R, dtype=U64)
+        for d, (ents, v) in enumerate(docs):
+            o = int(offsets[d])
+            for i, (k, a, c) in enumerate(ents):
+                keys[o + i], actors[o + i], counters[o + i] = k, a, c
+            vv[d * R:(d + 1) * R] = v
+        return AWSetBatch(R, offsets, keys, actors, counters, vv, counts if slack else None)
+
+    def live(self, d) -> int:
+        if self.counts is not None:
+            return int(self.counts[d])
+        return int(self.offsets[d + 1]) - int(self.offsets[d])
+
+    def doc(self, d):
+        """(entries [(key, actor, counter)], vv list) of doc d (host batch)."""
+        o, n = int(self.offsets[d]), self.live(d)
+        ents = list(zip(self.keys[o:o + n].tolist(), self.actors[o:o + n].tolist(), self.counters[o:o + n].tolist()))
+        return ents, self.vv[d * self.R:(d + 1) * self.R].tolist()
+
+    def live_slots(self) -> int:
+        if self.counts is not None:
+            return int(np.asarray(_np(self.counts, U32), dtype=np.uint64).sum())
+        o = _np(self.offsets, U32)
+        return int(o[-1]) - int(o[0])
+
+
+class OutBuffers:
+    """Output of a join/fold: n_docs docs, `slots` capacity, numpy or torch."""
+
+    def __init__(self, n_docs, R, slots, device=None):
+        self.R, self.n_docs, self.slots = int(R), int(n_docs), int(slots)
+        if device is None:
+            self.offsets = np.zeros(n_docs + 1, dtype=U32)
+            self.counts = np.zeros(n_docs, dtype=U32)
+            self.keys = np.zeros(max(slots, 1), dtype=U64)
+            self.actors = np.zeros(max(slots, 1), dtype=U32)
+            self.counters = np.zeros(max(slots, 1), dtype=U64)
+            self.vv = np.zeros(max(n_docs * R, 1), dtype=U64)
+        else:
+            import torch
+
+            e = lambda n, dt: torch.empty(max(n, 1), dtype=dt, device=device)  # noqa: E731
+            self.offsets = e(n_docs + 1, torch.int32)[: n_docs + 1]
+            self.counts = e(n_docs, torch.int32)[:n_docs]
+            self.keys = e(slots, torch.int64)
+            self.actors = e(slots, torch.int32)
+            self.counters = e(slots, torch.int64)
+            self.vv = e(n_docs * R, torch.int64)
+
+    def c(self) -> CAWSetOut:
+        return CAWSetOut(ptr(self.offsets), ptr(self.counts), ptr(self.keys), ptr(self.actors), ptr(self.counters),
+                         ptr(self.vv))
+
+    def as_batch(self) -> AWSetBatch:
+        return AWSetBatch(self.R, self.offsets, self.keys, self.actors, self.counters, self.vv, counts=self.counts)
+
+
+class SrcBatch:
+    """Ordered sources folded into each doc (AWSet or AWSetDelta states)."""
+
+    def __init__(self, R, doc_srcs, src_actor, vv, entry_off, keys, actors, counters,
+                 tomb_off=None, tkeys=None, tactors=None, tcounters=None):
+        self.R = int(R)
+        self.doc_srcs, self.src_actor, self.vv, self.entry_off = doc_srcs, src_actor, vv, entry_off
+        self.keys, self.actors, self.counters = keys, actors, counters
+        self.tomb_off, self.tkeys, self.tactors, self.tcounters = tomb_off, tkeys, tactors, tcounters
+
+    @property
+    def n_docs(self) -> int:
+        return int(self.doc_srcs.shape[0]) - 1
+
+    @property
+    def n_srcs(self) -> int:
+        return int(self.src_actor.shape[0])
+
+    def c(self) -> CSrcBatch:
+        return CSrcBatch(self.n_docs, self.R, ptr(self.doc_srcs), ptr(self.src_actor), ptr(self.vv),
+                         ptr(self.entry_off), ptr(self.keys), ptr(self.actors), ptr(self.counters),
+                         ptr(self.tomb_off), ptr(self.tkeys), ptr(self.tactors), ptr(self.tcounters))
+
+    _FIELDS = (("doc_srcs", U32), ("src_actor", U32), ("vv", U64), ("entry_off", U32), ("keys", U64),
+               ("actors", U32), ("counters", U64), ("tomb_off", U32), ("tkeys", U64), ("tactors", U32),
+               ("tcounters", U64))
+
+    def to(self, device) -> "SrcBatch":
+        return SrcBatch(self.R, *(_torch(getattr(self, f), device) for f, _ in self._FIELDS))
+
+    def numpy(self) -> "SrcBatch":
+        return SrcBatch(self.R, *(_np(getattr(self, f), dt) for f, dt in self._FIELDS))
+
+    @staticmethod
+    def from_lists(R, per_doc) -> "SrcBatch":
+        """per_doc[d] = list of sources (actor, vv, entries [(k,a,c)], tombstones [(k,a,c)] or None)."""
+        srcs = [s for lst in per_doc for s in lst]
+        doc_srcs = np.zeros(len(per_doc) + 1, dtype=U32)
+        np.cumsum([len(lst) for lst in per_doc], out=doc_srcs[1:])
+        ns = len(srcs)
+        src_actor = np.array([s[0] for s in srcs], dtype=U32).reshape(ns)
+        vv = np.zeros(max(ns * R, 1), dtype=U64)
+        entry_off = np.zeros(ns + 1, dtype=U32)
+        tomb_off = np.zeros(ns + 1, dtype=U32)
+        for i, s in enumerate(srcs):
+            vv[i * R:(i + 1) * R] = s[1]
+            entry_off[i + 1] = entry_off[i] + len(s[2])
+            tomb_off[i + 1] = tomb_off[i] + len(s[3] or [])
+        def flat(idx, off):
+            n = int(off[-1])
+            k, a, c = np.zeros(max(n, 1), U64), np.zeros(max(n, 1), U32), np.zeros(max(n, 1), U64)
+            for i, s in enumerate(srcs):
+                for j, (kk, aa, cc) in enumerate(s[idx] or []):
+                    k[off[i] + j], a[off[i] + j], c[off[i] + j] = kk, aa, cc
+            return k, a, c
+        keys, actors, counters = flat(2, entry_off)
+        tkeys, tactors, tcounters = flat(3, tomb_off)
+        return SrcBatch(R, doc_srcs, src_actor, vv, entry_off, keys, actors, counters,
+                        tomb_off, tkeys, tactors, tcounters)
+
+    def out_slots(self, dst: AWSetBatch) -> int:
+        eo = _np(self.entry_off, U32)
+        return int(_np(dst.offsets, U32)[-1]) + int(eo[-1])
+
+
+def c_ref(x):
+    return ctypes.byref(x)

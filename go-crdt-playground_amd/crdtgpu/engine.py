@@ -1,0 +1,101 @@
+"""Engine: one crdt_ctx (one per host thread), the batched merge entry points."""
+
+from __future__ import annotations
+
+import ctypes
+
+from . import abi
+from .abi import check
+from .batch import AWSetBatch, OutBuffers, SrcBatch, ptr
+
+
+def _stream(stream):
+    if stream is None:
+        return None
+    if hasattr(stream, "cuda_stream"):
+        return stream.cuda_stream
+    return int(stream)
+
+
+class Engine:
+    def __init__(self, device: int = 0):
+        self._lib = abi.lib()
+        h = ctypes.c_void_p()
+        check(self._lib.crdt_ctx_create(int(device), ctypes.byref(h)), "crdt_ctx_create")
+        self._ctx = h
+        self.device = device
+
+    def close(self):
+        if self._ctx:
+            self._lib.crdt_ctx_destroy(self._ctx)
+            self._ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    # -- workspace / errors ------------------------------------------------
+    def reserve(self, max_docs: int, max_fold_slots: int = 0):
+        check(self._lib.crdt_ctx_reserve(self._ctx, int(max_docs), int(max_fold_slots)), "crdt_ctx_reserve")
+
+    def sync(self, stream=None):
+        check(self._lib.crdt_ctx_sync(self._ctx, _stream(stream)), "crdt_ctx_sync")
+
+    # -- device-resident, asynchronous -------------------------------------
+    def join_async(self, dst: AWSetBatch, src: AWSetBatch, out: OutBuffers, stream=None):
+        d, s, o = dst.c(), src.c(), out.c()
+        check(self._lib.crdt_awset_join_async(self._ctx, ctypes.byref(d), ctypes.byref(s), ctypes.byref(o),
+                                              _stream(stream)), "crdt_awset_join_async")
+
+    def fold_async(self, mode: int, dst: AWSetBatch, srcs: SrcBatch, out: OutBuffers, stream=None):
+        d, s, o = dst.c(), srcs.c(), out.c()
+        check(self._lib.crdt_awset_fold_async(self._ctx, int(mode), ctypes.byref(d), ctypes.byref(s),
+                                              ctypes.byref(o), _stream(stream)), "crdt_awset_fold_async")
+
+    def vv_max_async(self, dst, src, n: int, stream=None):
+        check(self._lib.crdt_vv_max_async(self._ctx, ptr(dst), ptr(src), int(n), _stream(stream)),
+              "crdt_vv_max_async")
+
+    def causal_context_async(self, vv, n_docs: int, R: int, out, stream=None):
+        check(self._lib.crdt_causal_context_async(self._ctx, ptr(vv), int(n_docs), int(R), ptr(out),
+                                                  _stream(stream)), "crdt_causal_context_async")
+
+    def gen_pair_async(self, seed: int, n_docs: int, a: OutBuffers, b: OutBuffers, stream=None):
+        ca, cb = a.c(), b.c()
+        check(self._lib.crdt_gen_pair_async(self._ctx, int(seed), int(n_docs), ctypes.byref(ca), ctypes.byref(cb),
+                                            _stream(stream)), "crdt_gen_pair_async")
+
+    # -- host buffers, synchronous ----------------------------------------
+    def join(self, dst: AWSetBatch, src: AWSetBatch) -> OutBuffers:
+        dst, src = dst.numpy(), src.numpy()
+        out = OutBuffers(dst.n_docs, dst.R, int(dst.offsets[-1]) + int(src.offsets[-1]))
+        d, s, o = dst.c(), src.c(), out.c()
+        check(self._lib.crdt_awset_join_batch(self._ctx, ctypes.byref(d), ctypes.byref(s), ctypes.byref(o)),
+              "crdt_awset_join_batch")
+        return out
+
+    def fold(self, mode: int, dst: AWSetBatch, srcs: SrcBatch) -> OutBuffers:
+        dst, srcs = dst.numpy(), srcs.numpy()
+        out = OutBuffers(dst.n_docs, dst.R, srcs.out_slots(dst))
+        d, s, o = dst.c(), srcs.c(), out.c()
+        check(self._lib.crdt_awset_fold_batch(self._ctx, int(mode), ctypes.byref(d), ctypes.byref(s),
+                                              ctypes.byref(o)), "crdt_awset_fold_batch")
+        return out
+
+
+def validate(batch: AWSetBatch) -> int:
+    b = batch.numpy().c()
+    return abi.lib().crdt_validate_batch(ctypes.byref(b))
+
+
+def validate_src(srcs: SrcBatch) -> int:
+    s = srcs.numpy().c()
+    return abi.lib().crdt_validate_src_batch(ctypes.byref(s))

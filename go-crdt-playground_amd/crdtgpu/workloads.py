@@ -1,0 +1,78 @@
+"""Host restatement of the synthetic workloads and the algorithmic byte counts.
+
+``pair_docs`` recomputes, on the host, the states ``crdt_gen_pair_async``
+writes on the device (csrc/gen.hip), for any sample of document ids: GPU tests
+compare the two, and tests/test_workloads.py replays the same documents as
+reference op sequences (Add / Del / Merge) to show the states are reachable.
+
+Byte counts are the metric definitions of BASELINE.md / SURVEY.md 8d.
+"""
+
+from __future__ import annotations
+
+import numpy as np
+
+UNITS48 = np.array([1, 5, 7, 11, 13, 17, 19, 23, 25, 29, 31, 35, 37, 41, 43, 47], dtype=np.uint64)
+M64 = (1 << 64) - 1
+
+
+def splitmix64(x):
+    """Vectorised splitmix64 over a uint64 array."""
+    x = np.asarray(x, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        x = x + np.uint64(0x9E3779B97F4A7C15)
+        x = (x ^ (x >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        x = (x ^ (x >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        return x ^ (x >> np.uint64(31))
+
+
+def pair_fates(seed: int, d: int, X: int):
+    """Per base key u < 48 of replica X of doc d: 'del' | 're' | 'keep'."""
+    s = int(splitmix64(np.uint64(seed) ^ np.uint64(2 * d + X)))
+    mul, add = int(UNITS48[s & 15]), (s >> 4) % 48
+    readd = ((s >> 12) & 3) == 0
+    out = []
+    for u in range(48):
+        p = (mul * u + add) % 48
+        out.append("del" if p < 8 else ("re" if readd and 8 <= p < 16 else "keep"))
+    return out
+
+
+def pair_docs(seed: int, docs):
+    """Host copy of the pair workload for doc ids `docs`: two lists of (entries, vv)."""
+    A, B = [], []
+    for d in docs:
+        for X, dst in ((0, A), (1, B)):
+            fates = pair_fates(seed, d, X)
+            c0 = 48 if X == 0 else 0
+            ops = 0
+            ents = []
+            for u in range(48):
+                if fates[u] == "del":
+                    continue
+                if fates[u] == "re":
+                    ops += 1
+                    ents.append(((d << 8) | u, X, c0 + ops))
+                else:
+                    ents.append(((d << 8) | u, 0, u + 1))
+            n_re = ops
+            lo = 48 if X == 0 else 72
+            for r in range(24):
+                ents.append(((d << 8) | (lo + r), X, c0 + n_re + r + 1))
+            vv = [48 + n_re + 24, 0] if X == 0 else [48, n_re + 24]
+            dst.append((ents, vv))
+    return A, B
+
+
+def join_bytes(n_dst, n_src, n_out, R) -> int:
+    """Σ over docs of 20(n_dst + n_src + n_out) + 24R + 12."""
+    n_dst, n_src, n_out = (np.asarray(x, dtype=np.int64) for x in (n_dst, n_src, n_out))
+    return int(20 * (n_dst.sum() + n_src.sum() + n_out.sum()) + (24 * R + 12) * n_dst.size)
+
+
+def fold_bytes(n_dst, n_out, src_entries, src_tombs, n_srcs_total, R) -> int:
+    """Σ over docs of 20 n_dst + 8R + 4 + Σ_j [20 (c_j + x_j) + 8R + 12] + 20 n_out + 8R + 4."""
+    n_dst, n_out = np.asarray(n_dst, dtype=np.int64), np.asarray(n_out, dtype=np.int64)
+    per_doc = 20 * (n_dst.sum() + n_out.sum()) + (16 * R + 8) * n_dst.size
+    per_src = 20 * (int(src_entries) + int(src_tombs)) + (8 * R + 12) * int(n_srcs_total)
+    return int(per_doc + per_src)

@@ -1,0 +1,424 @@
+// C ABI of the engine (include/crdtgpu.h): context, validation, launches and
+// the synchronous host-buffer path used by the cgo drop-in.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdint>
+#include <cstring>
+#include <new>
+
+#include "../../include/crdtgpu.h"
+#include "crdt_device.hpp"
+
+namespace crdt {
+hipError_t launch_join(const BatchView& dst, const BatchView& src, const OutView& out, const Work& wk,
+                       uint32_t block_grid, hipStream_t stream);
+hipError_t launch_fold(int mode, const BatchView& dst, const SrcView& sb, const OutView& out, const Scratch& scr,
+                       const Work& wk, uint32_t block_grid, hipStream_t stream);
+hipError_t launch_vv_max(uint64_t* dst, const uint64_t* src, size_t n, hipStream_t stream);
+hipError_t launch_context(const uint64_t* vv, uint32_t n_docs, uint32_t R, uint64_t* part, uint32_t n_part,
+                          uint64_t* out, hipStream_t stream);
+hipError_t launch_gen_pair(uint64_t seed, uint32_t n_docs, const OutView& A, const OutView& B, hipStream_t stream);
+}  // namespace crdt
+
+using namespace crdt;
+
+namespace {
+
+constexpr uint32_t kCtxParts = 1024;
+
+// Device buffer that only grows.
+struct DevBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+    int reserve(size_t want) {
+        if (want <= bytes) return CRDT_OK;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        bytes = 0;
+        if (hipMalloc(&p, want) != hipSuccess) return CRDT_E_NOMEM;
+        bytes = want;
+        return CRDT_OK;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        bytes = 0;
+    }
+    template <typename T>
+    T* as(size_t byte_off = 0) const {
+        return reinterpret_cast<T*>(static_cast<char*>(p) + byte_off);
+    }
+};
+
+}  // namespace
+
+struct crdt_ctx {
+    int device = 0;
+    int n_cu = 256;
+    // [0,16): per-call counters {wl_count, wl_head, -, -} zeroed by every call;
+    // [16,20): status word, cleared by crdt_ctx_sync.
+    DevBuf ws;
+    DevBuf worklist;
+    DevBuf parts;
+    DevBuf scratch;  // fold block path ping-pong: keys | actors | counters
+    size_t scratch_slots = 0;
+    // staging for the *_batch host path
+    DevBuf stage[24];
+    hipStream_t stream = nullptr;
+};
+
+namespace {
+
+int hip_err(hipError_t e) { return e == hipSuccess ? CRDT_OK : CRDT_E_HIP; }
+
+int set_device(crdt_ctx* ctx) { return hip_err(hipSetDevice(ctx->device)); }
+
+uint32_t block_grid(const crdt_ctx* ctx) { return (uint32_t)ctx->n_cu * 2u; }
+
+Work make_work(crdt_ctx* ctx) {
+    Work w;
+    w.wl_count = ctx->ws.as<uint32_t>(0);
+    w.wl_head = ctx->ws.as<uint32_t>(4);
+    w.status = ctx->ws.as<uint32_t>(16);
+    w.worklist = ctx->worklist.as<uint32_t>();
+    return w;
+}
+
+int reserve_worklist(crdt_ctx* ctx, uint32_t n_docs) {
+    return ctx->worklist.reserve(std::max<size_t>((size_t)n_docs, 1) * sizeof(uint32_t));
+}
+
+int reserve_scratch(crdt_ctx* ctx, uint64_t slots) {
+    if (slots <= ctx->scratch_slots) return CRDT_OK;
+    int rc = ctx->scratch.reserve(slots * 20 + 64);
+    if (rc == CRDT_OK) ctx->scratch_slots = slots;
+    return rc;
+}
+
+BatchView view(const crdt_awset_batch* b) {
+    return BatchView{b->n_docs, b->R, b->offsets, b->counts, b->keys, b->actors, b->counters, b->vv};
+}
+
+OutView view(const crdt_awset_out* o) {
+    return OutView{o->offsets, o->counts, o->keys, o->actors, o->counters, o->vv};
+}
+
+SrcView view(const crdt_src_batch* s) {
+    return SrcView{s->n_docs,    s->R,       s->doc_srcs, s->src_actor, s->vv,    s->entry_off, s->keys,
+                   s->actors,    s->counters, s->tomb_off, s->tkeys,     s->tactors, s->tcounters};
+}
+
+bool batch_ptrs_ok(const crdt_awset_batch* b) {
+    return b && b->offsets && (b->n_docs == 0 || b->vv) && b->R > 0 && b->R <= CRDT_MAX_R;
+}
+
+bool out_ptrs_ok(const crdt_awset_out* o) {
+    return o && o->offsets && o->counts && o->keys && o->actors && o->counters && o->vv;
+}
+
+bool src_ptrs_ok(const crdt_src_batch* s) {
+    return s && s->doc_srcs && s->src_actor && s->entry_off && s->R > 0 && s->R <= CRDT_MAX_R &&
+           (!s->tomb_off || (s->tkeys && s->tactors && s->tcounters));
+}
+
+}  // namespace
+
+extern "C" {
+
+int crdt_abi_version(void) { return CRDTGPU_ABI_VERSION; }
+
+const char* crdt_strerror(int code) {
+    switch (code) {
+        case CRDT_OK: return "ok";
+        case CRDT_E_INVALID: return "invalid argument";
+        case CRDT_E_ACTOR_RANGE: return "dot actor == len(VersionVector): the reference panics (index out of range)";
+        case CRDT_E_UNSORTED: return "keys of a document are not strictly ascending";
+        case CRDT_E_CAPACITY: return "live count exceeds the document's slots";
+        case CRDT_E_HIP: return "HIP runtime error";
+        case CRDT_E_NOMEM: return "device allocation failed";
+        case CRDT_E_WORKSPACE: return "fold scratch too small: call crdt_ctx_reserve with the output slot count";
+        default: return "unknown error";
+    }
+}
+
+int crdt_ctx_create(int device, crdt_ctx** out) {
+    if (!out) return CRDT_E_INVALID;
+    *out = nullptr;
+    crdt_ctx* ctx = new (std::nothrow) crdt_ctx();
+    if (!ctx) return CRDT_E_NOMEM;
+    ctx->device = device;
+    int rc = set_device(ctx);
+    hipDeviceProp_t prop;
+    if (rc == CRDT_OK && hipGetDeviceProperties(&prop, device) == hipSuccess) ctx->n_cu = prop.multiProcessorCount;
+    if (rc == CRDT_OK) rc = ctx->ws.reserve(64);
+    if (rc == CRDT_OK) rc = hip_err(hipMemset(ctx->ws.p, 0, 64));
+    if (rc == CRDT_OK) rc = reserve_worklist(ctx, 1024);
+    if (rc == CRDT_OK) rc = ctx->parts.reserve((size_t)kCtxParts * CRDT_MAX_R * sizeof(uint64_t));
+    if (rc == CRDT_OK) rc = hip_err(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
+    if (rc != CRDT_OK) {
+        crdt_ctx_destroy(ctx);
+        return rc;
+    }
+    *out = ctx;
+    return CRDT_OK;
+}
+
+void crdt_ctx_destroy(crdt_ctx* ctx) {
+    if (!ctx) return;
+    (void)hipSetDevice(ctx->device);
+    if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    ctx->ws.release();
+    ctx->worklist.release();
+    ctx->parts.release();
+    ctx->scratch.release();
+    for (auto& b : ctx->stage) b.release();
+    delete ctx;
+}
+
+int crdt_ctx_reserve(crdt_ctx* ctx, uint32_t max_docs, uint64_t max_fold_slots) {
+    if (!ctx) return CRDT_E_INVALID;
+    int rc = set_device(ctx);
+    if (rc == CRDT_OK) rc = reserve_worklist(ctx, max_docs);
+    if (rc == CRDT_OK) rc = reserve_scratch(ctx, max_fold_slots);
+    return rc;
+}
+
+int crdt_ctx_sync(crdt_ctx* ctx, void* stream) {
+    if (!ctx) return CRDT_E_INVALID;
+    int rc = set_device(ctx);
+    if (rc != CRDT_OK) return rc;
+    hipStream_t s = (hipStream_t)stream;
+    if (hipStreamSynchronize(s) != hipSuccess) return CRDT_E_HIP;
+    uint32_t status = 0;
+    if (hipMemcpy(&status, ctx->ws.as<uint32_t>(16), sizeof(status), hipMemcpyDeviceToHost) != hipSuccess)
+        return CRDT_E_HIP;
+    if (status) {
+        if (hipMemset(ctx->ws.as<uint32_t>(16), 0, sizeof(uint32_t)) != hipSuccess) return CRDT_E_HIP;
+        if (status & kErrActorRange) return CRDT_E_ACTOR_RANGE;
+        if (status & kErrWorkspace) return CRDT_E_WORKSPACE;
+    }
+    return CRDT_OK;
+}
+
+int crdt_awset_join_async(crdt_ctx* ctx, const crdt_awset_batch* dst, const crdt_awset_batch* src,
+                          const crdt_awset_out* out, void* stream) {
+    if (!ctx || !batch_ptrs_ok(dst) || !batch_ptrs_ok(src) || !out_ptrs_ok(out)) return CRDT_E_INVALID;
+    if (dst->n_docs != src->n_docs || dst->R != src->R) return CRDT_E_INVALID;
+    int rc = set_device(ctx);
+    if (rc == CRDT_OK) rc = reserve_worklist(ctx, dst->n_docs);
+    if (rc != CRDT_OK) return rc;
+    hipStream_t s = (hipStream_t)stream;
+    if (hipMemsetAsync(ctx->ws.p, 0, 16, s) != hipSuccess) return CRDT_E_HIP;
+    return hip_err(launch_join(view(dst), view(src), view(out), make_work(ctx), block_grid(ctx), s));
+}
+
+int crdt_awset_fold_async(crdt_ctx* ctx, int mode, const crdt_awset_batch* dst, const crdt_src_batch* srcs,
+                          const crdt_awset_out* out, void* stream) {
+    if (!ctx || !batch_ptrs_ok(dst) || !src_ptrs_ok(srcs) || !out_ptrs_ok(out)) return CRDT_E_INVALID;
+    if (mode != CRDT_FOLD_AWSET && mode != CRDT_FOLD_DELTA) return CRDT_E_INVALID;
+    if (dst->n_docs != srcs->n_docs || dst->R != srcs->R) return CRDT_E_INVALID;
+    int rc = set_device(ctx);
+    if (rc == CRDT_OK) rc = reserve_worklist(ctx, dst->n_docs);
+    if (rc != CRDT_OK) return rc;
+    if (ctx->scratch_slots == 0 && reserve_scratch(ctx, 1) != CRDT_OK) return CRDT_E_NOMEM;
+    hipStream_t s = (hipStream_t)stream;
+    if (hipMemsetAsync(ctx->ws.p, 0, 16, s) != hipSuccess) return CRDT_E_HIP;
+    const size_t slots = ctx->scratch_slots;
+    Scratch scr{ctx->scratch.as<uint64_t>(0), ctx->scratch.as<uint32_t>(slots * 16), ctx->scratch.as<uint64_t>(slots * 8),
+                slots};
+    return hip_err(launch_fold(mode, view(dst), view(srcs), view(out), scr, make_work(ctx), block_grid(ctx), s));
+}
+
+int crdt_vv_max_async(crdt_ctx* ctx, uint64_t* dst, const uint64_t* src, size_t n, void* stream) {
+    if (!ctx || (n && (!dst || !src))) return CRDT_E_INVALID;
+    int rc = set_device(ctx);
+    if (rc != CRDT_OK) return rc;
+    return hip_err(launch_vv_max(dst, src, n, (hipStream_t)stream));
+}
+
+int crdt_causal_context_async(crdt_ctx* ctx, const uint64_t* vv, uint32_t n_docs, uint32_t R, uint64_t* out,
+                              void* stream) {
+    if (!ctx || !out || R == 0 || R > CRDT_MAX_R || (n_docs && !vv)) return CRDT_E_INVALID;
+    int rc = set_device(ctx);
+    if (rc != CRDT_OK) return rc;
+    uint32_t n_part = std::min<uint32_t>(kCtxParts, std::max<uint32_t>(1u, (n_docs + 255) / 256));
+    return hip_err(launch_context(vv, n_docs, R, ctx->parts.as<uint64_t>(), n_part, out, (hipStream_t)stream));
+}
+
+int crdt_gen_pair_async(crdt_ctx* ctx, uint64_t seed, uint32_t n_docs, const crdt_awset_out* a,
+                        const crdt_awset_out* b, void* stream) {
+    if (!ctx || !out_ptrs_ok(a) || !out_ptrs_ok(b)) return CRDT_E_INVALID;
+    if ((uint64_t)n_docs * 64ull >= (1ull << 32)) return CRDT_E_INVALID;
+    int rc = set_device(ctx);
+    if (rc != CRDT_OK) return rc;
+    return hip_err(launch_gen_pair(seed, n_docs, view(a), view(b), (hipStream_t)stream));
+}
+
+/* ---------------- validation (host) ---------------- */
+
+int crdt_validate_batch(const crdt_awset_batch* b) {
+    if (!b || !b->offsets || b->R == 0 || b->R > CRDT_MAX_R) return CRDT_E_INVALID;
+    if (b->n_docs && (!b->vv || ((b->offsets[b->n_docs] > b->offsets[0]) && (!b->keys || !b->actors || !b->counters))))
+        return CRDT_E_INVALID;
+    for (uint32_t d = 0; d < b->n_docs; d++) {
+        const uint32_t o = b->offsets[d], e = b->offsets[d + 1];
+        if (e < o) return CRDT_E_INVALID;
+        const uint32_t n = b->counts ? b->counts[d] : e - o;
+        if (n > e - o) return CRDT_E_CAPACITY;
+        for (uint32_t i = o + 1; i < o + n; i++)
+            if (b->keys[i] <= b->keys[i - 1]) return CRDT_E_UNSORTED;
+    }
+    return CRDT_OK;
+}
+
+int crdt_validate_src_batch(const crdt_src_batch* s) {
+    if (!src_ptrs_ok(s)) return CRDT_E_INVALID;
+    const uint32_t ns = s->doc_srcs[s->n_docs];
+    for (uint32_t d = 0; d < s->n_docs; d++)
+        if (s->doc_srcs[d + 1] < s->doc_srcs[d]) return CRDT_E_INVALID;
+    if (ns && !s->vv) return CRDT_E_INVALID;
+    for (uint32_t k = 0; k < ns; k++) {
+        const uint32_t o = s->entry_off[k], e = s->entry_off[k + 1];
+        if (e < o) return CRDT_E_INVALID;
+        for (uint32_t i = o + 1; i < e; i++)
+            if (s->keys[i] <= s->keys[i - 1]) return CRDT_E_UNSORTED;
+        if (s->tomb_off) {
+            const uint32_t to = s->tomb_off[k], te = s->tomb_off[k + 1];
+            if (te < to) return CRDT_E_INVALID;
+            for (uint32_t i = to + 1; i < te; i++)
+                if (s->tkeys[i] <= s->tkeys[i - 1]) return CRDT_E_UNSORTED;
+        }
+    }
+    return CRDT_OK;
+}
+
+/* ---------------- synchronous host-buffer path ---------------- */
+
+}  // extern "C"
+
+namespace {
+
+struct Stager {
+    crdt_ctx* ctx;
+    int next = 0;
+    int rc = CRDT_OK;
+    template <typename T>
+    T* put(const T* host, size_t n) {  // allocate + copy in (n elements)
+        if (rc != CRDT_OK) return nullptr;
+        DevBuf& b = ctx->stage[next++];
+        rc = b.reserve(std::max<size_t>(n, 1) * sizeof(T));
+        if (rc != CRDT_OK) return nullptr;
+        if (host && n && hipMemcpyAsync(b.p, host, n * sizeof(T), hipMemcpyHostToDevice, ctx->stream) != hipSuccess)
+            rc = CRDT_E_HIP;
+        return b.as<T>();
+    }
+    template <typename T>
+    T* room(size_t n) {
+        return put<T>(nullptr, n);
+    }
+};
+
+template <typename T>
+int get(T* host, const T* dev, size_t n, hipStream_t s) {
+    if (!n) return CRDT_OK;
+    return hip_err(hipMemcpyAsync(host, dev, n * sizeof(T), hipMemcpyDeviceToHost, s));
+}
+
+crdt_awset_batch stage_batch(Stager& st, const crdt_awset_batch* h) {
+    crdt_awset_batch d = *h;
+    const size_t slots = h->offsets[h->n_docs];
+    d.offsets = st.put(h->offsets, (size_t)h->n_docs + 1);
+    d.counts = h->counts ? st.put(h->counts, h->n_docs) : nullptr;
+    d.keys = st.put(h->keys, slots);
+    d.actors = st.put(h->actors, slots);
+    d.counters = st.put(h->counters, slots);
+    d.vv = st.put(h->vv, (size_t)h->n_docs * h->R);
+    return d;
+}
+
+crdt_awset_out stage_out(Stager& st, uint32_t n_docs, uint32_t R, size_t slots) {
+    crdt_awset_out o;
+    o.offsets = st.room<uint32_t>((size_t)n_docs + 1);
+    o.counts = st.room<uint32_t>(n_docs);
+    o.keys = st.room<uint64_t>(slots);
+    o.actors = st.room<uint32_t>(slots);
+    o.counters = st.room<uint64_t>(slots);
+    o.vv = st.room<uint64_t>((size_t)n_docs * R);
+    return o;
+}
+
+int fetch_out(const crdt_awset_out* h, const crdt_awset_out& d, uint32_t n_docs, uint32_t R, size_t slots,
+              hipStream_t s) {
+    int rc = get(h->offsets, d.offsets, (size_t)n_docs + 1, s);
+    if (rc == CRDT_OK) rc = get(h->counts, d.counts, n_docs, s);
+    if (rc == CRDT_OK) rc = get(h->keys, d.keys, slots, s);
+    if (rc == CRDT_OK) rc = get(h->actors, d.actors, slots, s);
+    if (rc == CRDT_OK) rc = get(h->counters, d.counters, slots, s);
+    if (rc == CRDT_OK) rc = get(h->vv, d.vv, (size_t)n_docs * R, s);
+    return rc;
+}
+
+}  // namespace
+
+extern "C" {
+
+int crdt_awset_join_batch(crdt_ctx* ctx, const crdt_awset_batch* dst, const crdt_awset_batch* src,
+                          const crdt_awset_out* out) {
+    if (!ctx || !out_ptrs_ok(out)) return CRDT_E_INVALID;
+    int rc = crdt_validate_batch(dst);
+    if (rc == CRDT_OK) rc = crdt_validate_batch(src);
+    if (rc != CRDT_OK) return rc;
+    if (dst->n_docs != src->n_docs || dst->R != src->R) return CRDT_E_INVALID;
+    if ((uint64_t)dst->offsets[dst->n_docs] + src->offsets[src->n_docs] >= (1ull << 32)) return CRDT_E_INVALID;
+    if ((rc = set_device(ctx)) != CRDT_OK) return rc;
+    Stager st{ctx};
+    crdt_awset_batch dd = stage_batch(st, dst), ds = stage_batch(st, src);
+    const size_t slots = (size_t)dst->offsets[dst->n_docs] + src->offsets[src->n_docs];
+    crdt_awset_out dout = stage_out(st, dst->n_docs, dst->R, slots);
+    if (st.rc != CRDT_OK) return st.rc;
+    rc = crdt_awset_join_async(ctx, &dd, &ds, &dout, ctx->stream);
+    if (rc == CRDT_OK) rc = fetch_out(out, dout, dst->n_docs, dst->R, slots, ctx->stream);
+    const int sync = crdt_ctx_sync(ctx, ctx->stream);
+    return rc != CRDT_OK ? rc : sync;
+}
+
+int crdt_awset_fold_batch(crdt_ctx* ctx, int mode, const crdt_awset_batch* dst, const crdt_src_batch* srcs,
+                          const crdt_awset_out* out) {
+    if (!ctx || !out_ptrs_ok(out)) return CRDT_E_INVALID;
+    int rc = crdt_validate_batch(dst);
+    if (rc == CRDT_OK) rc = crdt_validate_src_batch(srcs);
+    if (rc != CRDT_OK) return rc;
+    if (dst->n_docs != srcs->n_docs || dst->R != srcs->R) return CRDT_E_INVALID;
+    const uint32_t ns = srcs->doc_srcs[srcs->n_docs];
+    const uint64_t total = (uint64_t)dst->offsets[dst->n_docs] + srcs->entry_off[ns];
+    if (total >= (1ull << 32)) return CRDT_E_INVALID;
+    if ((rc = set_device(ctx)) != CRDT_OK) return rc;
+    if ((rc = reserve_scratch(ctx, total)) != CRDT_OK) return rc;
+    Stager st{ctx};
+    crdt_awset_batch dd = stage_batch(st, dst);
+    crdt_src_batch ds = *srcs;
+    const size_t ne = srcs->entry_off[ns];
+    const size_t nt = srcs->tomb_off ? srcs->tomb_off[ns] : 0;
+    ds.doc_srcs = st.put(srcs->doc_srcs, (size_t)srcs->n_docs + 1);
+    ds.src_actor = st.put(srcs->src_actor, ns);
+    ds.vv = st.put(srcs->vv, (size_t)ns * srcs->R);
+    ds.entry_off = st.put(srcs->entry_off, (size_t)ns + 1);
+    ds.keys = st.put(srcs->keys, ne);
+    ds.actors = st.put(srcs->actors, ne);
+    ds.counters = st.put(srcs->counters, ne);
+    if (srcs->tomb_off) {
+        ds.tomb_off = st.put(srcs->tomb_off, (size_t)ns + 1);
+        ds.tkeys = st.put(srcs->tkeys, nt);
+        ds.tactors = st.put(srcs->tactors, nt);
+        ds.tcounters = st.put(srcs->tcounters, nt);
+    }
+    crdt_awset_out dout = stage_out(st, dst->n_docs, dst->R, total);
+    if (st.rc != CRDT_OK) return st.rc;
+    rc = crdt_awset_fold_async(ctx, mode, &dd, &ds, &dout, ctx->stream);
+    if (rc == CRDT_OK) rc = fetch_out(out, dout, dst->n_docs, dst->R, total, ctx->stream);
+    const int sync = crdt_ctx_sync(ctx, ctx->stream);
+    return rc != CRDT_OK ? rc : sync;
+}
+
+}  // extern "C"

@@ -1,0 +1,154 @@
+// Device-side building blocks shared by the join and fold kernels (gfx950).
+//
+// The per-key rule these helpers serve is the reference's merge
+// (awset.go:107-161) and delta merge (awset-delta_test.go:51-166); see
+// DESIGN.md "Per-key rule" for how one rule covers both.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/crdtgpu.h"
+
+namespace crdt {
+
+constexpr int kWave = 64;
+
+// Device status bits (OR-ed into the context's status word).
+constexpr uint32_t kErrActorRange = 1u;
+constexpr uint32_t kErrWorkspace = 2u;  // fold scratch smaller than the output slots
+
+// Kernel-side view of an AWSet batch (same fields as crdt_awset_batch).
+struct BatchView {
+    uint32_t n_docs, R;
+    const uint32_t* offsets;
+    const uint32_t* counts;
+    const uint64_t* keys;
+    const uint32_t* actors;
+    const uint64_t* counters;
+    const uint64_t* vv;
+};
+
+struct OutView {
+    uint32_t* offsets;
+    uint32_t* counts;
+    uint64_t* keys;
+    uint32_t* actors;
+    uint64_t* counters;
+    uint64_t* vv;
+};
+
+struct SrcView {
+    uint32_t n_docs, R;
+    const uint32_t* doc_srcs;
+    const uint32_t* src_actor;
+    const uint64_t* vv;
+    const uint32_t* entry_off;
+    const uint64_t* keys;
+    const uint32_t* actors;
+    const uint64_t* counters;
+    const uint32_t* tomb_off;
+    const uint64_t* tkeys;
+    const uint32_t* tactors;
+    const uint64_t* tcounters;
+};
+
+// Scratch copy of the output slots (fold block path ping-pong), `slots` long.
+struct Scratch {
+    uint64_t* keys;
+    uint32_t* actors;
+    uint64_t* counters;
+    uint64_t slots;
+};
+
+// Workspace shared by the launches of one call.
+struct Work {
+    uint32_t* status;      // device status word (kErr* bits)
+    uint32_t* wl_count;    // number of docs pushed to the block-path worklist
+    uint32_t* wl_head;     // dequeue head of the block path
+    uint32_t* worklist;    // [n_docs]
+};
+
+__device__ __forceinline__ uint32_t live_count(const uint32_t* offsets, const uint32_t* counts, uint32_t d) {
+    return counts ? counts[d] : offsets[d + 1] - offsets[d];
+}
+
+// VersionVector.HasDot (crdt-misc.go:28-34) against a VV of length R held in
+// LDS.  actor > R: "never seen"; actor == R: the Go slice index panics, flagged.
+__device__ __forceinline__ bool has_dot(const uint64_t* vv, uint32_t R, uint32_t actor, uint64_t counter,
+                                        uint32_t& err) {
+    if (actor >= R) {
+        if (actor == R) err |= kErrActorRange;
+        return false;
+    }
+    return vv[actor] >= counter;
+}
+
+// VersionVector.Counter (crdt-misc.go:36-41).
+__device__ __forceinline__ uint64_t vv_counter(const uint64_t* vv, uint32_t R, uint32_t actor, uint32_t& err) {
+    if (actor >= R) {
+        if (actor == R) err |= kErrActorRange;
+        return 0;
+    }
+    return vv[actor];
+}
+
+// Intra-wave ordering of LDS traffic (all lanes of one wave).
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ uint32_t lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
+
+__device__ __forceinline__ uint64_t ballot(bool p) { return __ballot(p); }
+
+__device__ __forceinline__ uint32_t popc(uint64_t m) { return (uint32_t)__popcll(m); }
+
+// Bits [0, n) set, n in [0, 64].
+__device__ __forceinline__ uint64_t low_mask(uint32_t n) { return n >= 64 ? ~0ull : ((1ull << n) - 1ull); }
+
+// Number of elements of the sorted a[0..n) strictly less than key; n <= 2^LOG.
+template <int LOG>
+__device__ __forceinline__ uint32_t lower_bound_pow(const uint64_t* a, uint32_t n, uint64_t key) {
+    uint32_t pos = 0;
+#pragma unroll
+    for (int s = LOG; s >= 0; --s) {
+        uint32_t step = 1u << s;
+        if (pos + step <= n && a[pos + step - 1] < key) pos += step;
+    }
+    return pos;
+}
+
+// Generic lower bound for any n (global or LDS memory).
+__device__ __forceinline__ uint32_t lower_bound(const uint64_t* a, uint32_t n, uint64_t key) {
+    uint32_t lo = 0, hi = n;
+    while (lo < hi) {
+        uint32_t mid = (lo + hi) >> 1;
+        if (a[mid] < key)
+            lo = mid + 1;
+        else
+            hi = mid;
+    }
+    return lo;
+}
+
+// Wave-uniform value (forces a scalar register).
+template <typename T>
+__device__ __forceinline__ T uniform(T v) {
+    return (T)__builtin_amdgcn_readfirstlane((int)v);
+}
+
+__device__ __forceinline__ void flag_error(uint32_t* status, uint32_t err) {
+    // one atomic per wave that saw an error
+    uint64_t m = ballot(err != 0);
+    if (m) {
+        uint32_t e = err;
+        // OR across the wave via readlane of the first erring lane is enough:
+        // only one error kind exists.
+        if (lane_id() == (uint32_t)__builtin_ctzll(m)) atomicOr(status, e);
+    }
+}
+
+}  // namespace crdt

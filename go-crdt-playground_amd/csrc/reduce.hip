@@ -1,0 +1,80 @@
+// Version-vector reductions.
+//  * vv_max_kernel: dst[i] = max(dst[i], src[i]) -- (*VersionVector).Merge,
+//    crdt-misc.go:43-55, over equal-length vectors (R-padded).
+//  * causal-context summary: elementwise max over n_docs VVs of length R, the
+//    per-GPU clock summary that bench.py all-reduces (max, u64) across GPUs.
+//    Two launches: per-block partial maxima, then one block folds the partials
+//    (deterministic, no global atomics).
+#include "crdt_device.hpp"
+
+namespace crdt {
+
+__global__ void vv_max_kernel(uint64_t* __restrict__ dst, const uint64_t* __restrict__ src, size_t n) {
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+        const uint64_t a = dst[i], b = src[i];
+        dst[i] = a > b ? a : b;
+    }
+}
+
+// Thread t of a block handles actor r = t % R over docs t/R, t/R + NT/R, ...
+// (threads t >= (NT/R)*R idle).  Block partial -> part[block*R + r].
+template <int NT>
+__global__ __launch_bounds__(NT) void context_partial_kernel(const uint64_t* __restrict__ vv, uint32_t n_docs,
+                                                             uint32_t R, uint64_t* __restrict__ part) {
+    __shared__ uint64_t red[NT];
+    const uint32_t t = threadIdx.x;
+    const uint32_t per = NT / R;  // docs per block-stride
+    const uint32_t r = t % R, lane_doc = t / R;
+    uint64_t m = 0;
+    if (lane_doc < per) {
+        const size_t stride = (size_t)gridDim.x * per;
+        for (size_t d = (size_t)blockIdx.x * per + lane_doc; d < n_docs; d += stride) {
+            const uint64_t v = vv[d * R + r];
+            m = v > m ? v : m;
+        }
+    }
+    red[t] = m;
+    __syncthreads();
+    if (t < R) {
+        uint64_t acc = 0;
+        for (uint32_t q = 0; q < per; ++q) {
+            const uint64_t v = red[q * R + t];
+            acc = v > acc ? v : acc;
+        }
+        part[(size_t)blockIdx.x * R + t] = acc;
+    }
+}
+
+__global__ void context_final_kernel(const uint64_t* __restrict__ part, uint32_t n_part, uint32_t R,
+                                     uint64_t* __restrict__ out) {
+    const uint32_t r = threadIdx.x;
+    if (r >= R) return;
+    uint64_t acc = 0;
+    for (uint32_t b = 0; b < n_part; ++b) {
+        const uint64_t v = part[(size_t)b * R + r];
+        acc = v > acc ? v : acc;
+    }
+    out[r] = acc;
+}
+
+constexpr int kCtxNT = 256;
+
+hipError_t launch_vv_max(uint64_t* dst, const uint64_t* src, size_t n, hipStream_t stream) {
+    if (n == 0) return hipSuccess;
+    size_t grid = (n + 255) / 256;
+    if (grid > 4096) grid = 4096;
+    hipLaunchKernelGGL(vv_max_kernel, dim3((uint32_t)grid), dim3(256), 0, stream, dst, src, n);
+    return hipGetLastError();
+}
+
+// part must hold n_part*R u64; n_part <= caller's bound.
+hipError_t launch_context(const uint64_t* vv, uint32_t n_docs, uint32_t R, uint64_t* part, uint32_t n_part,
+                          uint64_t* out, hipStream_t stream) {
+    hipLaunchKernelGGL((context_partial_kernel<kCtxNT>), dim3(n_part), dim3(kCtxNT), 0, stream, vv, n_docs, R, part);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(context_final_kernel, dim3(1), dim3(64), 0, stream, part, n_part, R, out);
+    return hipGetLastError();
+}
+
+}  // namespace crdt

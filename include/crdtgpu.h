@@ -1,0 +1,166 @@
+/*
+ * crdtgpu.h -- C ABI of the MI355X batched AWSet merge engine.
+ *
+ * The reference (rsms/go-crdt-playground, package crdt) has no FFI: its merge
+ * path is a Go method set called in-process.  Each entry point below replaces
+ * one of those methods, applied to a whole batch of independent documents at
+ * once; a cgo package with the reference's types calls them.
+ *
+ *   crdt_awset_join_async / crdt_awset_join_batch
+ *       replace (*AWSet).Merge / merge                 awset.go:103-161
+ *   crdt_awset_fold_async / crdt_awset_fold_batch, mode CRDT_FOLD_AWSET
+ *       replace an ordered sequence of (*AWSet).Merge  awset.go:103-161
+ *   crdt_awset_fold_async / crdt_awset_fold_batch, mode CRDT_FOLD_DELTA
+ *       replace (*AWSetDelta).Merge with MakeDeltaMergeData, deltaMerge and
+ *       the (no-op) gcDeleted                          awset-delta_test.go:51-166
+ *   crdt_vv_max_async
+ *       replaces (*VersionVector).Merge                crdt-misc.go:43-55
+ *   crdt_causal_context_async
+ *       the elementwise max over many version vectors (no reference
+ *       counterpart: the per-GPU summary reduced across GPUs by RCCL)
+ *
+ * HasDot (crdt-misc.go:28-34) and Counter (:36-41) run inside the kernels.
+ *
+ * Encoding (SoA, all little-endian):
+ *   entry  = key id u64 + dot actor u32 + dot counter u64   (20 B)
+ *   VV     = R x u64 per state, R identical for every state of a call
+ *   doc d of a batch owns the slots [offsets[d], offsets[d+1]); its live
+ *   entries are the first counts[d] of them (counts == NULL: all slots live),
+ *   keys strictly ascending.  Strings are interned to key ids by the caller.
+ *
+ * HasDot / Counter with actor == R index one past the reference's slice and
+ * panic in Go; here the call returns CRDT_E_ACTOR_RANGE instead (outputs then
+ * undefined).  actor > R is "never seen" (false / 0), as in the reference.
+ *
+ * Output: doc d of a join is written at out offset dst.offsets[d] +
+ * src.offsets[d] (capacity = both inputs' capacities), its live count to
+ * out->counts[d], its slot bounds to out->offsets[d] (n_docs+1 values) and its
+ * VV to out->vv.  Entries come out sorted by key.  No scan over documents is
+ * needed, so one launch finishes the batch, and the output is directly a valid
+ * input batch for the next merge.
+ *
+ * Threading: one crdt_ctx per host thread; *_async calls are ordered on the
+ * given HIP stream; crdt_ctx_sync returns device-side errors.  Device buffers
+ * passed to *_async are caller-owned (device-resident, e.g. torch tensors).
+ * The *_batch calls take host buffers and are synchronous.
+ */
+#ifndef CRDTGPU_H
+#define CRDTGPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CRDTGPU_ABI_VERSION 1
+
+/* status codes */
+#define CRDT_OK 0
+#define CRDT_E_INVALID (-1)     /* null pointer, R==0 or R>CRDT_MAX_R, bad sizes       */
+#define CRDT_E_ACTOR_RANGE (-2) /* HasDot/Counter at actor == R: reference panics     */
+#define CRDT_E_UNSORTED (-3)    /* keys of a doc not strictly ascending (validation)  */
+#define CRDT_E_CAPACITY (-4)    /* a doc's live count exceeds its slots               */
+#define CRDT_E_HIP (-5)         /* HIP runtime error                                   */
+#define CRDT_E_NOMEM (-6)       /* device allocation failed                            */
+#define CRDT_E_WORKSPACE (-7)   /* fold block path needs crdt_ctx_reserve(max_fold_slots) */
+
+#define CRDT_MAX_R 64 /* version-vector length limit (one wave lane per actor) */
+
+/* fold modes */
+#define CRDT_FOLD_AWSET 0 /* each step = (*AWSet).Merge: tombstones ignored       */
+#define CRDT_FOLD_DELTA 1 /* each step = (*AWSetDelta).Merge                       */
+
+typedef struct crdt_ctx crdt_ctx;
+
+/* A batch of AWSet states (read-only view). */
+typedef struct {
+    uint32_t n_docs;
+    uint32_t R;
+    const uint32_t* offsets;  /* [n_docs+1] slot bounds                          */
+    const uint32_t* counts;   /* [n_docs] live entries, or NULL = all slots live */
+    const uint64_t* keys;     /* [offsets[n_docs]]                              */
+    const uint32_t* actors;   /* [offsets[n_docs]]                              */
+    const uint64_t* counters; /* [offsets[n_docs]]                              */
+    const uint64_t* vv;       /* [n_docs*R]                                     */
+} crdt_awset_batch;
+
+/* Output of a join or fold (written). */
+typedef struct {
+    uint32_t* offsets;  /* [n_docs+1]                          */
+    uint32_t* counts;   /* [n_docs]                            */
+    uint64_t* keys;     /* capacity = Σ input slots            */
+    uint32_t* actors;
+    uint64_t* counters;
+    uint64_t* vv;       /* [n_docs*R]                          */
+} crdt_awset_out;
+
+/*
+ * Ordered source states folded into each dst doc (AWSet or AWSetDelta
+ * states).  Doc d receives sources [doc_srcs[d], doc_srcs[d+1]) in that order.
+ * Source s: replica actor src_actor[s] (AWSetDelta.Actor, read by the path
+ * select of awset-delta_test.go:53), VV vv[s*R..], entries
+ * [entry_off[s], entry_off[s+1]) and tombstones (AWSetDelta.Deleted)
+ * [tomb_off[s], tomb_off[s+1]), each sorted by key.  tomb_off may be NULL.
+ * Fold output capacity of doc d: dst slots + Σ its sources' entry slots, at
+ * offset dst.offsets[d] + entry_off[doc_srcs[d]].
+ */
+typedef struct {
+    uint32_t n_docs;
+    uint32_t R;
+    const uint32_t* doc_srcs;   /* [n_docs+1]  */
+    const uint32_t* src_actor;  /* [n_srcs]    */
+    const uint64_t* vv;         /* [n_srcs*R]  */
+    const uint32_t* entry_off;  /* [n_srcs+1]  */
+    const uint64_t* keys;
+    const uint32_t* actors;
+    const uint64_t* counters;
+    const uint32_t* tomb_off;   /* [n_srcs+1] or NULL */
+    const uint64_t* tkeys;
+    const uint32_t* tactors;
+    const uint64_t* tcounters;
+} crdt_src_batch;
+
+/* ---- context ---------------------------------------------------------- */
+int crdt_ctx_create(int device, crdt_ctx** out);
+void crdt_ctx_destroy(crdt_ctx* ctx);
+/* Pre-size workspaces so that *_async calls never allocate (graph capture). */
+int crdt_ctx_reserve(crdt_ctx* ctx, uint32_t max_docs, uint64_t max_fold_slots);
+/* Wait for `stream`, return (and clear) the first device-side error. */
+int crdt_ctx_sync(crdt_ctx* ctx, void* stream);
+const char* crdt_strerror(int code);
+int crdt_abi_version(void);
+
+/* ---- device-resident, asynchronous on a HIP stream (NULL = default) ---- */
+int crdt_awset_join_async(crdt_ctx* ctx, const crdt_awset_batch* dst, const crdt_awset_batch* src,
+                          const crdt_awset_out* out, void* stream);
+int crdt_awset_fold_async(crdt_ctx* ctx, int mode, const crdt_awset_batch* dst, const crdt_src_batch* srcs,
+                          const crdt_awset_out* out, void* stream);
+/* dst[i] = max(dst[i], src[i]) for i < n (u64). */
+int crdt_vv_max_async(crdt_ctx* ctx, uint64_t* dst, const uint64_t* src, size_t n, void* stream);
+/* out[r] = max over d < n_docs of vv[d*R + r]  (the per-GPU causal-context summary). */
+int crdt_causal_context_async(crdt_ctx* ctx, const uint64_t* vv, uint32_t n_docs, uint32_t R, uint64_t* out,
+                              void* stream);
+
+/* ---- synthetic workloads (bench / GPU tests; not part of a merge) ----------
+ * "pair" (BASELINE config 2): n_docs documents x 2 replicas (A actor 0, B
+ * actor 1), R = 2, 64 live entries each in 64 slots per doc; reachable states
+ * (formulas: go-crdt-playground_amd/csrc/gen.hip).  a/b need n_docs*64 slots. */
+int crdt_gen_pair_async(crdt_ctx* ctx, uint64_t seed, uint32_t n_docs, const crdt_awset_out* a,
+                        const crdt_awset_out* b, void* stream);
+
+/* ---- host buffers, synchronous: copies in, runs, copies out ------------- */
+int crdt_awset_join_batch(crdt_ctx* ctx, const crdt_awset_batch* dst, const crdt_awset_batch* src,
+                          const crdt_awset_out* out);
+int crdt_awset_fold_batch(crdt_ctx* ctx, int mode, const crdt_awset_batch* dst, const crdt_src_batch* srcs,
+                          const crdt_awset_out* out);
+
+/* ---- host-side validation of a packed batch (no GPU) -------------------- */
+int crdt_validate_batch(const crdt_awset_batch* b);
+int crdt_validate_src_batch(const crdt_src_batch* s);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CRDTGPU_H */

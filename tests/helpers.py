@@ -1,0 +1,114 @@
+"""Shared test helpers: case generators and conversions between the map-based
+oracle (oracle/awset_ref.py), SoA batches and the C oracle."""
+
+from __future__ import annotations
+
+import os
+import random
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "go-crdt-playground_amd")
+for p in (ROOT, PKG):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+from crdtgpu.batch import AWSetBatch, SrcBatch  # noqa: E402
+from oracle import awset_ref as ref  # noqa: E402
+
+GOLDEN = os.path.join(ROOT, "tests", "golden", "kat_scenarios.json")
+
+
+# ---------------------------------------------------------------- conversion
+
+def intern(states):
+    keys = set()
+    for s in states:
+        keys.update(s.Entries)
+        if getattr(s, "Deleted", None):
+            keys.update(s.Deleted)
+    return {k: i for i, k in enumerate(sorted(keys))}
+
+
+def ents(m, ids):
+    return sorted((ids[k], d.actor, d.counter) for k, d in (m or {}).items())
+
+
+def pad(vv, R):
+    return list(vv) + [0] * (R - len(vv))
+
+
+def snap_entries(snap, ids):
+    return sorted((ids[k], a, c) for k, a, c in snap["entries"])
+
+
+def out_doc(out, d, R):
+    o, n = int(out.offsets[d]), int(out.counts[d])
+    e = list(zip(out.keys[o:o + n].tolist(), out.actors[o:o + n].tolist(), out.counters[o:o + n].tolist()))
+    return e, out.vv[d * R:(d + 1) * R].tolist()
+
+
+def outs_equal(a, b, n_docs, R):
+    """Bit-exact comparison of two outputs (entries of every doc, VVs, slot bounds)."""
+    for d in range(n_docs):
+        if out_doc(a, d, R) != out_doc(b, d, R):
+            return d
+    if list(np.asarray(a.offsets[: n_docs + 1])) != list(np.asarray(b.offsets[: n_docs + 1])):
+        return -1
+    return None
+
+
+# ---------------------------------------------------------------- generators
+
+KEYS = ["k%03d" % i for i in range(200)]
+
+
+def random_history(rng: random.Random, R: int, n_ops: int, n_keys: int, delta: bool):
+    """R replicas doing random Add / Del / Merge; returns the replicas."""
+    cls = ref.AWSetDelta if delta else ref.AWSet
+    reps = [cls(a, ref.VersionVector([0] * R)) for a in range(R)]
+    keys = KEYS[:n_keys]
+    for _ in range(n_ops):
+        r = rng.randrange(R)
+        op = rng.random()
+        if op < 0.45:
+            reps[r].Add(*rng.sample(keys, rng.randint(1, 3)))
+        elif op < 0.7:
+            reps[r].Del(*rng.sample(keys, rng.randint(1, 3)))
+        else:
+            o = rng.randrange(R)
+            if o != r:
+                reps[r].Merge(reps[o])
+    return reps
+
+
+def random_state(rng: random.Random, R: int, n: int, universe: int, max_counter: int, actor_hi=None):
+    """Arbitrary (not necessarily reachable) AWSet state: keys, dots and VV at random."""
+    actor_hi = R - 1 if actor_hi is None else actor_hi
+    keys = sorted(rng.sample(range(universe), n))
+    e = [(k, rng.randint(0, actor_hi), rng.randint(1, max_counter)) for k in keys]
+    vv = [rng.randint(0, max_counter) for _ in range(R)]
+    return e, vv
+
+
+def ref_state(entries, vv, actor=0, cls=None, deleted=None):
+    """SoA doc -> map-based oracle state (keys named by their id)."""
+    cls = cls or ref.AWSet
+    s = cls(actor, ref.VersionVector(vv), {"%012d" % k: ref.Dot(a, c) for k, a, c in entries})
+    if deleted is not None:
+        s.Deleted = {"%012d" % k: ref.Dot(a, c) for k, a, c in deleted} or None
+    return s
+
+
+def ref_entries(s):
+    return sorted((int(k), d.actor, d.counter) for k, d in s.Entries.items())
+
+
+def batch_of(R, docs, slack=0):
+    return AWSetBatch.from_docs(R, docs, slack=slack)
+
+
+def src_batch_of(R, per_doc):
+    return SrcBatch.from_lists(R, per_doc)

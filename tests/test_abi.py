@@ -1,0 +1,92 @@
+"""CPU: the C-ABI library loads, exports every symbol include/crdtgpu.h
+declares, and its host-only entry points (validation, strerror) behave.  No
+compute call is made here (no GPU in this container)."""
+
+import ctypes
+
+import numpy as np
+import pytest
+
+import crdtgpu
+from crdtgpu import abi
+from crdtgpu.batch import AWSetBatch, SrcBatch
+from helpers import batch_of, src_batch_of
+
+
+def test_exports_every_header_symbol():
+    names = crdtgpu.header_functions()
+    assert len(names) >= 15
+    lib = ctypes.CDLL(crdtgpu.LIB_PATH)
+    missing = [n for n in names if not hasattr(lib, n)]
+    assert not missing, missing
+
+
+def test_abi_version_and_strerror():
+    assert crdtgpu.lib().crdt_abi_version() == 1
+    for code in (0, -1, -2, -3, -4, -5, -6, -7):
+        assert crdtgpu.strerror(code) != "unknown error"
+    assert "panic" in crdtgpu.strerror(crdtgpu.CRDT_E_ACTOR_RANGE)
+
+
+def test_struct_layouts():
+    # pointer-sized fields after two u32: offsets at 8 (no padding surprises)
+    assert ctypes.sizeof(abi.CAWSetBatch) == 8 + 6 * 8
+    assert ctypes.sizeof(abi.CAWSetOut) == 6 * 8
+    assert ctypes.sizeof(abi.CSrcBatch) == 8 + 11 * 8
+    assert abi.CAWSetBatch.offsets.offset == 8
+
+
+def test_validate_batch():
+    good = batch_of(2, [([(1, 0, 1), (4, 1, 2)], [1, 2]), ([], [0, 0])])
+    assert crdtgpu.validate(good) == 0
+    unsorted = batch_of(2, [([(4, 0, 1), (1, 1, 2)], [1, 2])])
+    assert crdtgpu.validate(unsorted) == crdtgpu.CRDT_E_UNSORTED
+    dup = batch_of(2, [([(4, 0, 1), (4, 1, 2)], [1, 2])])
+    assert crdtgpu.validate(dup) == crdtgpu.CRDT_E_UNSORTED
+    over = batch_of(2, [([(1, 0, 1)], [1, 0])], slack=1)
+    over.counts[0] = 5
+    assert crdtgpu.validate(over) == crdtgpu.CRDT_E_CAPACITY
+    wide = AWSetBatch(65, good.offsets, good.keys, good.actors, good.counters, np.zeros(130, np.uint64))
+    assert crdtgpu.validate(wide) == crdtgpu.CRDT_E_INVALID
+
+
+def test_validate_src_batch():
+    ok = src_batch_of(2, [[(0, [1, 0], [(1, 0, 1)], [(2, 0, 1)])], []])
+    assert crdtgpu.validate_src(ok) == 0
+    bad = src_batch_of(2, [[(0, [1, 0], [(3, 0, 1), (1, 0, 1)], [])]])
+    assert crdtgpu.validate_src(bad) == crdtgpu.CRDT_E_UNSORTED
+    badt = src_batch_of(2, [[(0, [1, 0], [], [(3, 0, 1), (3, 0, 2)])]])
+    assert crdtgpu.validate_src(badt) == crdtgpu.CRDT_E_UNSORTED
+
+
+def test_product_has_no_cpu_fallback():
+    """The product package must not import the oracle or ship a CPU merge."""
+    import os
+    import re
+
+    pkg = os.path.dirname(crdtgpu.__file__)
+    for fn in os.listdir(pkg):
+        if fn.endswith(".py"):
+            src = open(os.path.join(pkg, fn)).read()
+            assert not re.search(r"\boracle\b", src.replace("oracle/", "")), fn
+
+
+def test_batch_roundtrip_numpy():
+    b = batch_of(3, [([(1, 0, 1), (9, 2, 7)], [1, 0, 7]), ([(2, 1, 1)], [0, 1, 0])])
+    assert b.n_docs == 2 and b.live(0) == 2 and b.live(1) == 1
+    assert b.doc(0) == ([(1, 0, 1), (9, 2, 7)], [1, 0, 7])
+    s = SrcBatch.from_lists(3, [[(1, [0, 1, 0], [(2, 1, 1)], None)], []])
+    assert s.n_docs == 2 and s.n_srcs == 1 and s.out_slots(b) == 4
+
+
+def test_engine_needs_a_gpu_or_works():
+    try:
+        import torch
+
+        has_gpu = torch.cuda.is_available()
+    except Exception:  # pragma: no cover
+        has_gpu = False
+    if has_gpu:
+        pytest.skip("GPU present: covered by -m gpu")
+    with pytest.raises(crdtgpu.CrdtError):
+        crdtgpu.Engine(0)

@@ -1,0 +1,321 @@
+"""GPU parity: the HIP kernels, called through the C ABI, against the C oracle.
+
+Bit-exact on every document: entries (keys, dot actors, dot counters), live
+counts, slot bounds and version vectors.  Covers the wave path (<= 64 entries
+per side), the block path (larger documents), empty and ragged documents, the
+64/65 boundary, the actor == len(vv) panic, ordered AWSet folds, AWSetDelta
+folds (first contact, pruning, no-op, tombstones, re-adds, LDS overflow
+hand-off), the device-side workload generator, and the config-2 size with
+size-independent properties.
+"""
+
+import json
+import random
+
+import numpy as np
+import pytest
+
+import crdtgpu
+from crdtgpu import CRDT_FOLD_AWSET, CRDT_FOLD_DELTA, workloads
+from crdtgpu.batch import OutBuffers
+from helpers import GOLDEN, batch_of, out_doc, outs_equal, random_state, snap_entries, src_batch_of
+from oracle import oracle
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def torch():
+    import torch as t
+
+    assert t.cuda.is_available(), "GPU tests need a HIP device"
+    return t
+
+
+@pytest.fixture(scope="module")
+def eng(torch):
+    e = crdtgpu.Engine(0)
+    yield e
+    e.close()
+
+
+def host_out(out, torch):
+    torch.cuda.synchronize()
+    h = OutBuffers(out.n_docs, out.R, 0)
+    for f in ("offsets", "counts", "keys", "actors", "counters", "vv"):
+        a = getattr(out, f).cpu().numpy()
+        setattr(h, f, a.view(np.uint32 if a.dtype == np.int32 else np.uint64))
+    return h
+
+
+def assert_same(got, want, n_docs, R):
+    bad = outs_equal(got, want, n_docs, R)
+    if bad is not None:
+        raise AssertionError("doc %s differs:\n gpu    %s\n oracle %s" % (
+            bad, out_doc(got, bad, R) if bad >= 0 else got.offsets[:8],
+            out_doc(want, bad, R) if bad >= 0 else want.offsets[:8]))
+
+
+def join_case(rng, n_docs, R, size_fn, universe, max_c, actor_hi=None):
+    dsts, srcs = [], []
+    for _ in range(n_docs):
+        dsts.append(random_state(rng, R, size_fn(), universe, max_c, actor_hi))
+        srcs.append(random_state(rng, R, size_fn(), universe, max_c, actor_hi))
+    return batch_of(R, dsts), batch_of(R, srcs)
+
+
+# ---------------------------------------------------------------- golden
+
+def test_golden_merges_on_gpu(eng):
+    g = json.load(open(GOLDEN))
+    n = 0
+    for sc in g["scenarios"]:
+        for m in sc["merges"]:
+            keys = sorted({e[0] for s in (m["dst"], m["src"], m["out"]) for e in s["entries"] + s.get("deleted", [])})
+            ids = {k: i for i, k in enumerate(keys)}
+            R = len(m["dst"]["vv"])
+            dst = batch_of(R, [(snap_entries(m["dst"], ids), m["dst"]["vv"])])
+            if sc["kind"] == "awset":
+                out = eng.join(dst, batch_of(R, [(snap_entries(m["src"], ids), m["src"]["vv"])]))
+            else:
+                s = m["src"]
+                dele = sorted((ids[k], a, c) for k, a, c in s["deleted"])
+                out = eng.fold(CRDT_FOLD_DELTA, dst, src_batch_of(R, [[(s["actor"], s["vv"], snap_entries(s, ids),
+                                                                        dele)]]))
+            e, vv = out_doc(out, 0, R)
+            assert e == snap_entries(m["out"], ids), (sc["name"], m["dst_name"], m["src_name"])
+            assert vv == m["out"]["vv"]
+            n += 1
+    assert n == 23
+
+
+# ---------------------------------------------------------------- join
+
+@pytest.mark.parametrize("R,maxn,universe", [(2, 64, 100), (3, 64, 70), (16, 40, 200), (64, 64, 128)])
+def test_join_wave_path_random(eng, R, maxn, universe):
+    rng = random.Random(R * 1000 + maxn)
+    dst, src = join_case(rng, 3000, R, lambda: rng.randint(0, maxn), universe, 9)
+    rc, want = oracle.join(dst, src)
+    assert rc == 0
+    assert_same(eng.join(dst, src), want, dst.n_docs, R)
+
+
+def test_join_boundary_sizes(eng):
+    rng = random.Random(11)
+    R = 2
+    sizes = [(0, 0), (0, 64), (64, 0), (64, 64), (63, 64), (64, 65), (65, 64), (65, 65), (1, 200), (200, 1),
+             (128, 0), (0, 129), (1000, 1000), (4097, 10), (3, 5000)]
+    dsts = [random_state(rng, R, a, 12000, 20) for a, _ in sizes]
+    srcs = [random_state(rng, R, b, 12000, 20) for _, b in sizes]
+    dst, src = batch_of(R, dsts), batch_of(R, srcs)
+    rc, want = oracle.join(dst, src)
+    assert rc == 0
+    assert_same(eng.join(dst, src), want, dst.n_docs, R)
+
+
+def test_join_block_path_large_random(eng):
+    rng = random.Random(12)
+    R = 4
+    dst, src = join_case(rng, 64, R, lambda: rng.choice([65, 300, 1023, 1024, 1025, 2500, 7000]), 20000, 30)
+    rc, want = oracle.join(dst, src)
+    assert rc == 0
+    assert_same(eng.join(dst, src), want, dst.n_docs, R)
+
+
+def test_join_mixed_sizes_device_async(eng, torch):
+    """Device-resident inputs with counts < slots (slack), through the async ABI."""
+    rng = random.Random(13)
+    R = 2
+    sz = lambda: rng.choice([0, 1, 7, 33, 64, 64, 65, 150])  # noqa: E731
+    dsts = [random_state(rng, R, sz(), 400, 12) for _ in range(2000)]
+    srcs = [random_state(rng, R, sz(), 400, 12) for _ in range(2000)]
+    dst, src = batch_of(R, dsts, slack=3), batch_of(R, srcs, slack=1)
+    rc, want = oracle.join(dst, src)
+    assert rc == 0
+    dev = torch.device("cuda:0")
+    dd, ds = dst.to(dev), src.to(dev)
+    out = OutBuffers(dst.n_docs, R, int(dst.offsets[-1]) + int(src.offsets[-1]), device=dev)
+    s = torch.cuda.current_stream()
+    eng.join_async(dd, ds, out, stream=s)
+    eng.sync(s)
+    assert_same(host_out(out, torch), want, dst.n_docs, R)
+
+
+def test_join_actor_range_error(eng):
+    R = 2
+    dst = batch_of(R, [([(1, 0, 1)], [1, 0]), ([(1, 2, 1)], [1, 1])])
+    src = batch_of(R, [([], [0, 0]), ([], [1, 1])])
+    with pytest.raises(crdtgpu.CrdtError) as ei:
+        eng.join(dst, src)
+    assert ei.value.code == crdtgpu.CRDT_E_ACTOR_RANGE
+    # the status is cleared afterwards, and actor > R is legal ("never seen")
+    rc, want = oracle.join(batch_of(R, [([(1, 5, 1)], [1, 1])]), batch_of(R, [([], [1, 1])]))
+    got = eng.join(batch_of(R, [([(1, 5, 1)], [1, 1])]), batch_of(R, [([], [1, 1])]))
+    assert rc == 0
+    assert_same(got, want, 1, R)
+
+
+def test_join_actor_range_error_block_path(eng):
+    R = 2
+    big = [(k, 0, 1) for k in range(100)] + [(1000, 2, 1)]
+    with pytest.raises(crdtgpu.CrdtError) as ei:
+        eng.join(batch_of(R, [(big, [1, 0])]), batch_of(R, [([], [5, 5])]))
+    assert ei.value.code == crdtgpu.CRDT_E_ACTOR_RANGE
+
+
+# ---------------------------------------------------------------- fold
+
+def fold_case(rng, n_docs, R, dst_n, n_src, src_n, tomb_n, universe, max_c, delta):
+    dsts, per_doc = [], []
+    for _ in range(n_docs):
+        dsts.append(random_state(rng, R, dst_n(), universe, max_c))
+        chain = []
+        for _ in range(n_src()):
+            e, vv = random_state(rng, R, src_n(), universe, max_c)
+            t = random_state(rng, R, tomb_n(), universe, max_c)[0] if delta else []
+            chain.append((rng.randrange(R), vv, e, t))
+        per_doc.append(chain)
+    return batch_of(R, dsts), src_batch_of(R, per_doc)
+
+
+@pytest.mark.parametrize("mode", [CRDT_FOLD_AWSET, CRDT_FOLD_DELTA])
+def test_fold_wave_path_random(eng, mode):
+    rng = random.Random(20 + mode)
+    R = 4
+    dst, srcs = fold_case(rng, 3000, R, lambda: rng.randint(0, 64), lambda: rng.randint(0, 10),
+                          lambda: rng.randint(0, 8), lambda: rng.randint(0, 3), 120, 8, mode == CRDT_FOLD_DELTA)
+    rc, want = oracle.fold(mode, dst, srcs)
+    assert rc == 0
+    assert_same(eng.fold(mode, dst, srcs), want, dst.n_docs, R)
+
+
+@pytest.mark.parametrize("mode", [CRDT_FOLD_AWSET, CRDT_FOLD_DELTA])
+def test_fold_block_path_and_overflow(eng, mode):
+    """Docs that start above CAP, grow above CAP mid-fold, or carry > 64 entries/tombstones per source."""
+    rng = random.Random(30 + mode)
+    R = 3
+    dst, srcs = fold_case(rng, 200, R, lambda: rng.choice([10, 100, 127, 128, 129, 600]), lambda: rng.randint(0, 6),
+                          lambda: rng.choice([5, 40, 64, 65, 300]), lambda: rng.choice([0, 2, 64, 65, 200]), 5000, 50,
+                          mode == CRDT_FOLD_DELTA)
+    rc, want = oracle.fold(mode, dst, srcs)
+    assert rc == 0
+    assert_same(eng.fold(mode, dst, srcs), want, dst.n_docs, R)
+
+
+def test_delta_fold_noop_and_first_contact(eng):
+    R = 2
+    # dst has seen actor 1 up to 5: src (actor 1) entries covered, no tombstones -> no-op, VV untouched
+    dst = batch_of(R, [([(1, 0, 1)], [1, 5]), ([(1, 0, 1)], [1, 0]), ([(1, 0, 1), (2, 1, 1)], [1, 5])])
+    per = [[(1, [9, 5], [(3, 1, 4)], [])],              # no-op
+           [(1, [9, 5], [(3, 1, 4)], [(1, 0, 9)])],     # first contact: tombstone ignored, (A 1) removed (9>=1)
+           [(1, [1, 6], [(3, 1, 6)], [(2, 1, 6)])]]     # delta: add (B 6), tombstone removes key 2
+    srcs = src_batch_of(R, per)
+    rc, want = oracle.fold(CRDT_FOLD_DELTA, dst, srcs)
+    assert rc == 0
+    got = eng.fold(CRDT_FOLD_DELTA, dst, srcs)
+    assert_same(got, want, 3, R)
+    assert out_doc(got, 0, R) == ([(1, 0, 1)], [1, 5])
+    assert out_doc(got, 1, R) == ([(3, 1, 4)], [9, 5])
+    assert out_doc(got, 2, R) == ([(1, 0, 1), (3, 1, 6)], [1, 6])
+
+
+def test_delta_fold_actor_range(eng):
+    R = 2
+    with pytest.raises(crdtgpu.CrdtError) as ei:
+        eng.fold(CRDT_FOLD_DELTA, batch_of(R, [([], [1, 1])]), src_batch_of(R, [[(2, [1, 1], [], [])]]))
+    assert ei.value.code == crdtgpu.CRDT_E_ACTOR_RANGE
+
+
+# ---------------------------------------------------------------- reductions
+
+def test_causal_context_and_vv_max(eng, torch):
+    rng = np.random.default_rng(3)
+    dev = torch.device("cuda:0")
+    for n_docs, R in [(1, 1), (5, 2), (1000, 16), (300001, 8), (77, 64)]:
+        vv = rng.integers(0, 2**63, size=n_docs * R, dtype=np.uint64)
+        want = oracle.causal_context(vv, n_docs, R)
+        dv = torch.from_numpy(vv.view(np.int64)).to(dev)
+        out = torch.zeros(R, dtype=torch.int64, device=dev)
+        eng.causal_context_async(dv, n_docs, R, out)
+        eng.sync()
+        assert out.cpu().numpy().view(np.uint64).tolist() == want.tolist()
+    a = rng.integers(0, 2**64 - 1, size=1000, dtype=np.uint64)
+    b = rng.integers(0, 2**64 - 1, size=1000, dtype=np.uint64)
+    da, db = torch.from_numpy(a.view(np.int64)).to(dev), torch.from_numpy(b.view(np.int64)).to(dev)
+    eng.vv_max_async(da, db, 1000)
+    eng.sync()
+    assert (da.cpu().numpy().view(np.uint64) == np.maximum(a, b)).all()
+
+
+# ---------------------------------------------------------------- workload + config 2
+
+def gen_pair(eng, torch, n_docs, seed):
+    dev = torch.device("cuda:0")
+    A = OutBuffers(n_docs, 2, n_docs * 64, device=dev)
+    B = OutBuffers(n_docs, 2, n_docs * 64, device=dev)
+    eng.gen_pair_async(seed, n_docs, A, B)
+    eng.sync()
+    return A, B
+
+
+def test_gen_pair_matches_host_restatement(eng, torch):
+    A, B = gen_pair(eng, torch, 5000, 0x5EED)
+    ha, hb = host_out(A, torch), host_out(B, torch)
+    docs = list(range(0, 5000, 37)) + [4999]
+    wa, wb = workloads.pair_docs(0x5EED, docs)
+    for i, d in enumerate(docs):
+        assert out_doc(ha, d, 2) == wa[i]
+        assert out_doc(hb, d, 2) == wb[i]
+
+
+def test_config2_full_size(eng, torch):
+    """1,048,576 docs x 2 replicas x 64 entries, both directions, on the device.
+    Exact against the oracle on a doc sample; size-independent properties on all docs."""
+    n = 1 << 20
+    A, B = gen_pair(eng, torch, n, 0x5EED)
+    dev = torch.device("cuda:0")
+    a, b = A.as_batch(), B.as_batch()
+    oab = OutBuffers(n, 2, 2 * n * 64, device=dev)
+    oba = OutBuffers(n, 2, 2 * n * 64, device=dev)
+    eng.join_async(a, b, oab)
+    eng.join_async(b, a, oba)
+    eng.sync()
+    # sample: exact vs the oracle on host-regenerated inputs
+    sample = sorted(set(random.Random(1).sample(range(n), 3000)) | {0, n - 1})
+    wa, wb = workloads.pair_docs(0x5EED, sample)
+    rc, want_ab = oracle.join(batch_of(2, wa), batch_of(2, wb))
+    assert rc == 0
+    rc, want_ba = oracle.join(batch_of(2, wb), batch_of(2, wa))
+    assert rc == 0
+    hab, hba = host_out(oab, torch), host_out(oba, torch)
+    for i, d in enumerate(sample):
+        assert out_doc(hab, d, 2) == out_doc(want_ab, i, 2), d
+        assert out_doc(hba, d, 2) == out_doc(want_ba, i, 2), d
+    # all docs: slot bounds, element-set symmetry (A<-B and B<-A hold the same keys), VV = max
+    offs = hab.offsets.astype(np.int64)
+    assert (offs == np.arange(n + 1, dtype=np.int64) * 128).all()
+    assert (hab.counts == hba.counts).all()
+    mask = np.zeros(hab.keys.shape[0], dtype=bool)
+    cnt = hab.counts.astype(np.int64)
+    starts = offs[:-1]
+    idx = np.repeat(starts, cnt) + (np.arange(cnt.sum()) - np.repeat(np.cumsum(cnt) - cnt, cnt))
+    mask[idx] = True
+    assert (hab.keys[mask] == hba.keys[mask]).all()
+    k = hab.keys[idx].astype(np.uint64)
+    same_doc = np.repeat(np.arange(n), cnt)
+    inner = same_doc[1:] == same_doc[:-1]
+    assert (k[1:][inner] > k[:-1][inner]).all(), "keys not strictly ascending inside a doc"
+    va = host_out(A, torch).vv.reshape(n, 2)
+    vb = host_out(B, torch).vv.reshape(n, 2)
+    assert (hab.vv.reshape(n, 2) == np.maximum(va, vb)).all()
+    # idempotence: X <- X == X on the whole output
+    ob = oab.as_batch()
+    oxx = OutBuffers(n, 2, 4 * n * 64, device=dev)
+    eng.join_async(ob, ob, oxx)
+    eng.sync()
+    hxx = host_out(oxx, torch)
+    assert (hxx.counts == hab.counts).all()
+    idx2 = np.repeat(hxx.offsets[:-1].astype(np.int64), cnt) + (idx - np.repeat(starts, cnt))
+    assert (hxx.keys[idx2] == hab.keys[idx]).all()
+    assert (hxx.actors[idx2] == hab.actors[idx]).all()
+    assert (hxx.counters[idx2] == hab.counters[idx]).all()

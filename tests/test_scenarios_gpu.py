@@ -1,0 +1,179 @@
+"""GPU: the reference's scenario tests, replayed through the host mirror of the
+Go API (crdtgpu.awset) whose Merge runs on the device.  Each test reads like
+its Go counterpart (awset_test.go, awset-delta_test.go); the final states are
+also compared, dots and clocks included, with tests/golden/kat_scenarios.json."""
+
+import json
+
+import pytest
+
+from crdtgpu.awset import AWSet, AWSetDelta, DeltaMergeBatch, Dot, FoldBatch, MergeBatch, VersionVector
+from helpers import GOLDEN
+
+pytestmark = pytest.mark.gpu
+
+
+def init(cls=AWSet):
+    return cls(0, [0, 0]), cls(1, [0, 0])
+
+
+def assert_entries(s, *values):
+    assert s.SortedValues() == sorted(values)
+
+
+def golden_final(name):
+    for sc in json.load(open(GOLDEN))["scenarios"]:
+        if sc["name"].startswith(name):
+            return sc["final"]
+    raise KeyError(name)
+
+
+def assert_golden(name, **reps):
+    fin = golden_final(name)
+    for r, s in reps.items():
+        want = fin[r]
+        assert list(s.VersionVector) == want["vv"], r
+        assert sorted((k, d.Actor, d.Counter) for k, d in s.Entries.items()) == [tuple(e) for e in want["entries"]], r
+
+
+def test_AWSetXXX():  # awset_test.go:10-29
+    A, B = init()
+    A.Add("A", "B", "C")
+    B.Add("A", "B", "C")
+    A.Merge(B)
+    B.Merge(A)
+    assert_entries(A, "A", "B", "C")
+    assert_entries(B, "A", "B", "C")
+    A.Del("B")
+    B.Add("B")
+    B.Merge(A)
+    A.Merge(B)
+    assert_entries(A, "A", "B", "C")
+    assert_entries(B, "A", "B", "C")  # concurrent writer wins
+    assert_golden("KAT-1", A=A, B=B)
+
+
+def test_AWSet():  # awset_test.go:31-83
+    A, B = init()
+    assert_entries(A)
+    assert_entries(B)
+    A.Add("Shelly")
+    assert_entries(A, "Shelly")
+    B.Merge(A)
+    assert_entries(B, "Shelly")
+    B.Add("Bob", "Phil", "Pete")
+    A.Merge(B)
+    assert_entries(A, "Shelly", "Bob", "Phil", "Pete")
+    A.Del("Phil")
+    A.Add("Bob")
+    A.Add("Anna")
+    assert_entries(A, "Shelly", "Bob", "Pete", "Anna")
+    B.Merge(A)
+    assert_entries(B, "Shelly", "Bob", "Pete", "Anna")
+    A.Del("Bob", "Pete")
+    B.Del("Bob", "Shelly")
+    A.Merge(B)
+    B.Merge(A)
+    assert_entries(A, "Anna")
+    assert_entries(B, "Anna")
+    A.Add("A", "B", "C")
+    A.Del("A")
+    A.Add("A")
+    B.Merge(A)
+    assert_entries(A, "Anna", "A", "B", "C")
+    assert_entries(B, "Anna", "A", "B", "C")
+    assert_golden("KAT-2", A=A, B=B)
+
+
+def test_AWSetConcurrentAddWinsOverDelete():  # awset_test.go:85-122
+    A, B = init()
+    A.Add("Anne", "Bob")
+    B.Add("Anne")
+    A2, B2 = A.Clone(), B.Clone()
+    B2.Add("Bob")
+    A2.Del("Bob")
+    B2.Merge(A2)
+    A2.Merge(B2)
+    assert_entries(B2, "Anne", "Bob")  # writer wins
+    assert_entries(A2, "Anne", "Bob")
+    B.Add("Bob")
+    B.Merge(A)
+    A.Del("Bob")
+    B.Merge(A)
+    A.Merge(B)
+    assert_entries(B, "Anne")
+    assert_entries(A, "Anne")
+    assert_golden("KAT-3", A=A, B=B, **{"A'": A2, "B'": B2})
+
+
+def test_AWSetCommutativity():  # awset_test.go:124-154
+    A, B = init()
+    A.Add("Shelly", "Bob", "Pete", "Anna")
+    B.Add("Shelly", "Bob", "Pete", "Anna")
+    A.Del("Anna")
+    B.Add("Anna")
+    want = ["Shelly", "Bob", "Pete", "Anna"]
+    A2, B2 = A.Clone(), B.Clone()
+    B2.Merge(A2)
+    A2.Merge(B2)
+    assert_entries(A2, *want)
+    assert_entries(B2, *want)
+    A.Merge(B)
+    B.Merge(A)
+    assert_entries(A, *want)
+    assert_entries(B, *want)
+    assert_golden("KAT-4", A=A, B=B, **{"A'": A2, "B'": B2})
+
+
+def test_AWSetDelta():  # awset-delta_test.go:168-189
+    A, B = init(AWSetDelta)
+    A.Add("A", "B")
+    B.Add("A", "C")
+    A.Merge(B)
+    B.Merge(A)
+    assert_entries(A, "A", "B", "C")
+    assert_entries(B, "A", "B", "C")
+    A.Del("B")
+    A.Add("D", "E")
+    B.Add("E")
+    B.Merge(A)
+    assert_entries(B, "A", "C", "D", "E")
+    A.Merge(B)
+    assert_entries(A, "A", "C", "D", "E")
+    assert A.VersionVector == [5, 2]  # the no-op delta leaves A's clock alone
+    assert_golden("KAT-5", A=A, B=B)
+
+
+def test_VersionVector():  # crdt-misc_test.go:5-28
+    A, B = VersionVector([1, 1, 0, 4]), VersionVector([2, 0, 3, 0])
+    A.Merge(B)
+    assert A == [2, 1, 3, 4]
+    B.Merge(A)
+    assert B == [2, 1, 3, 4]
+
+
+def test_batch_entry_points():
+    """MergeBatch / FoldBatch / DeltaMergeBatch over many independent docs at once."""
+    dsts, srcs = [], []
+    for i in range(50):
+        a, b = AWSet(0, [0, 0]), AWSet(1, [0, 0])
+        a.Add(*["x%d" % j for j in range(i % 7)])
+        b.Add(*["x%d" % j for j in range(i % 5)])
+        dsts.append(a)
+        srcs.append(b)
+    MergeBatch(dsts, srcs)
+    for i, a in enumerate(dsts):
+        assert a.SortedValues() == sorted("x%d" % j for j in range(max(i % 7, i % 5)))
+        assert list(a.VersionVector) == [i % 7, i % 5]
+    # fold: dst <- b1 <- b2 in order
+    d = AWSet(0, [0, 0, 0])
+    b1, b2 = AWSet(1, [0, 0, 0]), AWSet(2, [0, 0, 0])
+    b1.Add("p", "q")
+    b2.Add("q")
+    FoldBatch([d], [[b1, b2]])
+    assert d.Entries == {"p": Dot(1, 1), "q": Dot(2, 1)}
+    # delta fold
+    x, y = AWSetDelta(0, [0, 0]), AWSetDelta(1, [0, 0])
+    y.Add("k")
+    DeltaMergeBatch([x], [[y]])
+    assert x.Entries == {"k": Dot(1, 1)} and list(x.VersionVector) == [0, 1]

@@ -1,0 +1,60 @@
+"""CPU: the synthetic "pair" workload (BASELINE config 2) is a set of
+reachable states -- replaying its definition through the reference semantics
+(map-based oracle: Add / Merge / Del in the stated order) yields exactly the
+states the generator formulas produce -- and the byte counts follow 8d."""
+
+import pytest
+
+from crdtgpu import workloads
+from helpers import ref
+
+
+def replay_pair(seed, d):
+    """The op history that defines doc d of the pair workload."""
+    name = lambda u: (d << 8) | u  # noqa: E731
+    A = ref.AWSet(0, ref.VersionVector([0, 0]))
+    B = ref.AWSet(1, ref.VersionVector([0, 0]))
+    A.Add(*[name(u) for u in range(48)])  # base, dots (A, u+1)
+    B.Merge(A)
+    for X, rep, new in ((0, A, range(48, 72)), (1, B, range(72, 96))):
+        fates = workloads.pair_fates(seed, d, X)
+        rep.Del(*[name(u) for u in range(48) if fates[u] == "del"])
+        ops = [u for u in range(48) if fates[u] == "re"] + list(new)
+        for u in sorted(ops):
+            rep.Add(name(u))
+    return A, B
+
+
+def as_doc(s):
+    return sorted((k, dt.actor, dt.counter) for k, dt in s.Entries.items()), list(s.VersionVector)
+
+
+@pytest.mark.parametrize("seed", [0x5EED, 1, 12345])
+def test_pair_workload_is_reachable(seed):
+    docs = [0, 1, 2, 3, 7, 1000, 123456, 1048575]
+    A, B = workloads.pair_docs(seed, docs)
+    for i, d in enumerate(docs):
+        a, b = replay_pair(seed, d)
+        assert A[i] == as_doc(a)
+        assert B[i] == as_doc(b)
+        assert len(A[i][0]) == 64 and len(B[i][0]) == 64
+
+
+def test_pair_workload_mix():
+    """~25% of replicas re-add; deletes are exactly 8 per replica."""
+    readd = 0
+    for d in range(400):
+        for X in (0, 1):
+            f = workloads.pair_fates(0x5EED, d, X)
+            assert f.count("del") == 8
+            readd += "re" in f
+    assert 120 < readd < 280
+
+
+def test_byte_formulas():
+    # one join of 64+64 -> 96 at R=2 is 20*224 + 24*2 + 12 = 4540 B
+    assert workloads.join_bytes([64], [64], [96], 2) == 4540
+    # delta fold, one doc: 20*64 + 8R+4 + [20*(8+2) + 8R+12]*10 + 20*n_out + 8R+4
+    R = 16
+    want = 20 * 64 + 8 * R + 4 + 10 * (20 * 10 + 8 * R + 12) + 20 * 100 + 8 * R + 4
+    assert workloads.fold_bytes([64], [100], 80, 20, 10, R) == want
