@@ -66,11 +66,36 @@ def header_functions(path: str = HEADER_PATH):
     return sorted(set(re.findall(r"^\s*(?:int|void|const char\*)\s+(crdt_\w+)\s*\(", text, flags=re.M)))
 
 
+def hip_runtimes_mapped():
+    """Distinct libamdhip64 files mapped into this process."""
+    out = set()
+    try:
+        with open("/proc/self/maps") as f:
+            for line in f:
+                if "libamdhip64" in line:
+                    out.add(os.path.realpath(line.split()[-1]))
+    except OSError:
+        pass
+    return sorted(out)
+
+
 def _load():
+    # PyTorch (the host's device-memory / stream / RCCL plumbing) bundles its
+    # own HIP runtime with the same soname (libamdhip64.so.7).  Loading torch
+    # first makes our NEEDED entry bind to that already-loaded runtime, so torch
+    # streams and allocations are native handles for this library; loading us
+    # first would put two HIP/HSA runtimes in one process.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     if not os.path.exists(LIB_PATH):
         raise ImportError("libcrdtgpu.so not built at %s: run `python -c 'import __graft_entry__ as g; g.build()'`"
                           % LIB_PATH)
     lib = ctypes.CDLL(LIB_PATH)
+    rts = hip_runtimes_mapped()
+    if len(rts) > 1:
+        raise ImportError("two HIP runtimes mapped into one process: %s" % rts)
     P = ctypes.POINTER
     sig = {
         "crdt_abi_version": (ctypes.c_int, []),

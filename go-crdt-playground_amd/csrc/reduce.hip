@@ -45,16 +45,31 @@ __global__ __launch_bounds__(NT) void context_partial_kernel(const uint64_t* __r
     }
 }
 
-__global__ void context_final_kernel(const uint64_t* __restrict__ part, uint32_t n_part, uint32_t R,
-                                     uint64_t* __restrict__ out) {
-    const uint32_t r = threadIdx.x;
-    if (r >= R) return;
-    uint64_t acc = 0;
-    for (uint32_t b = 0; b < n_part; ++b) {
-        const uint64_t v = part[(size_t)b * R + r];
-        acc = v > acc ? v : acc;
+// One block folds the n_part partials: thread t takes actor t % R over
+// partial rows t / R, t / R + NT / R, ...; then R threads fold the LDS row.
+template <int NT>
+__global__ __launch_bounds__(NT) void context_final_kernel(const uint64_t* __restrict__ part, uint32_t n_part,
+                                                           uint32_t R, uint64_t* __restrict__ out) {
+    __shared__ uint64_t red[NT];
+    const uint32_t t = threadIdx.x;
+    const uint32_t per = NT / R;
+    const uint32_t r = t % R, row = t / R;
+    uint64_t m = 0;
+    if (row < per)
+        for (uint32_t b = row; b < n_part; b += per) {
+            const uint64_t v = part[(size_t)b * R + r];
+            m = v > m ? v : m;
+        }
+    red[t] = m;
+    __syncthreads();
+    if (t < R) {
+        uint64_t acc = 0;
+        for (uint32_t q = 0; q < per; ++q) {
+            const uint64_t v = red[q * R + t];
+            acc = v > acc ? v : acc;
+        }
+        out[t] = acc;
     }
-    out[r] = acc;
 }
 
 constexpr int kCtxNT = 256;
@@ -73,7 +88,7 @@ hipError_t launch_context(const uint64_t* vv, uint32_t n_docs, uint32_t R, uint6
     hipLaunchKernelGGL((context_partial_kernel<kCtxNT>), dim3(n_part), dim3(kCtxNT), 0, stream, vv, n_docs, R, part);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(context_final_kernel, dim3(1), dim3(64), 0, stream, part, n_part, R, out);
+    hipLaunchKernelGGL((context_final_kernel<kCtxNT>), dim3(1), dim3(kCtxNT), 0, stream, part, n_part, R, out);
     return hipGetLastError();
 }
 

@@ -90,3 +90,8 @@ def test_engine_needs_a_gpu_or_works():
         pytest.skip("GPU present: covered by -m gpu")
     with pytest.raises(crdtgpu.CrdtError):
         crdtgpu.Engine(0)
+
+
+def test_single_hip_runtime_in_process():
+    """torch and libcrdtgpu.so must share one HIP runtime (torch streams are passed in)."""
+    assert len(abi.hip_runtimes_mapped()) <= 1, abi.hip_runtimes_mapped()

@@ -24,3 +24,6 @@ if [ "${PROFILE:-1}" = 1 ]; then
   cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
   run prof 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$TAG -o run -- python3 bench.py --no-cpu-baseline ${BENCH_ARGS:-}
 fi
+if [ "${PMC:-0}" = 1 ]; then
+  run pmc 900 bash tools/pmc.sh
+fi

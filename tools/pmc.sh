@@ -1,0 +1,28 @@
+#!/bin/bash
+# PMC passes for the join kernel, one counter group per rocprofv3 run (gfx950
+# slot limits), plus the known-byte calibration run.  GPU box only.
+set -u
+cd "$(dirname "$0")/.."
+TAG=${TAG:-r01}
+OUT=gpurun_out/pmc_$TAG
+mkdir -p "$OUT"
+cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
+BENCH="python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline ${BENCH_ARGS:-}"
+pass() {
+  local name=$1; shift
+  timeout -k 10 -s KILL 120 rocprofv3 --pmc "$@" --output-format csv -d "$OUT/$name" -o run -- $BENCH > "$OUT/$name.log" 2>&1
+  local rc=$?; echo "[pmc $name] rc=$rc"; [ $rc -eq 0 ] || { tail -20 "$OUT/$name.log"; exit $rc; }
+}
+cpass() {
+  local name=$1; shift
+  timeout -k 10 -s KILL 120 rocprofv3 --pmc "$@" --output-format csv -d "$OUT/$name" -o run -- python3 tools/calib.py > "$OUT/$name.log" 2>&1
+  local rc=$?; echo "[pmc $name] rc=$rc"; [ $rc -eq 0 ] || { tail -20 "$OUT/$name.log"; exit $rc; }
+}
+pass fetch FETCH_SIZE
+pass write WRITE_SIZE
+pass sq SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU
+pass lds SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_SALU SQ_INSTS_SMEM SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS GRBM_GUI_ACTIVE GRBM_COUNT
+pass tcc TCC_HIT_sum TCC_MISS_sum
+cpass calib_fetch FETCH_SIZE
+cpass calib_write WRITE_SIZE
+python3 tools/traffic.py "$OUT" --docs ${DOCS:-1048576} > "$OUT/summary.txt" && cat "$OUT/summary.txt"

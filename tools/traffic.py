@@ -1,0 +1,74 @@
+#!/usr/bin/env python3
+"""Summarise the rocprofv3 PMC passes of tools/pmc.sh.
+
+Per kernel: mean counter value per dispatch.  HBM traffic of the join kernel is
+FETCH_SIZE + WRITE_SIZE (KiB units), corrected by the known-byte calibration run
+(tools/calib.py: vv_max_kernel, 8 B per lane): correction = known bytes /
+counted bytes, applied per direction (the guide's gfx950 note: FETCH_SIZE counts
+half of a wide coalesced stream; other widths must be calibrated).
+Writes <dir>/traffic.json and, with --emit, profiles/traffic_latest.json.
+"""
+import argparse
+import csv
+import glob
+import json
+import os
+from collections import defaultdict
+
+
+def load(d):
+    vals = defaultdict(lambda: defaultdict(list))  # kernel -> counter -> [per dispatch]
+    for fn in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+        per = defaultdict(float)
+        names = {}
+        with open(fn) as f:
+            for row in csv.DictReader(f):
+                key = (row.get("Dispatch_Id") or row.get("Correlation_Id"), row["Counter_Name"])
+                per[key] += float(row["Counter_Value"])
+                names[key[0]] = row["Kernel_Name"]
+        for (disp, cname), v in per.items():
+            vals[names[disp]][cname].append(v)
+    return vals
+
+
+def short(k):
+    return k.split("(")[0].replace("void ", "").replace("crdt::", "")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("dir")
+    ap.add_argument("--docs", type=int, default=1 << 20)
+    ap.add_argument("--emit", action="store_true")
+    a = ap.parse_args()
+    out = {}
+    for sub in sorted(os.listdir(a.dir)):
+        p = os.path.join(a.dir, sub)
+        if not os.path.isdir(p):
+            continue
+        for k, cs in load(p).items():
+            for c, v in cs.items():
+                out.setdefault(short(k), {})[c] = sum(v) / len(v)
+    for k in sorted(out):
+        print(k)
+        for c, v in sorted(out[k].items()):
+            print("   %-24s %.6g" % (c, v))
+    cal = out.get("vv_max_kernel", {})
+    N = 64 << 20
+    fcorr = (16 * N) / (cal["FETCH_SIZE"] * 1024) if cal.get("FETCH_SIZE") else None
+    wcorr = (8 * N) / (cal["WRITE_SIZE"] * 1024) if cal.get("WRITE_SIZE") else None
+    j = next((v for k, v in out.items() if k.startswith("join_wave_kernel")), {})
+    res = {"docs": a.docs, "kernel": "join_wave_kernel<4>", "fetch_correction": fcorr, "write_correction": wcorr}
+    if j.get("FETCH_SIZE") is not None and j.get("WRITE_SIZE") is not None:
+        rd = j["FETCH_SIZE"] * 1024 * (fcorr or 1.0)
+        wr = j["WRITE_SIZE"] * 1024 * (wcorr or 1.0)
+        res.update({"fetch_bytes_raw": j["FETCH_SIZE"] * 1024, "write_bytes_raw": j["WRITE_SIZE"] * 1024,
+                    "read_bytes": rd, "write_bytes": wr, "hbm_bytes_per_launch": rd + wr})
+    print(json.dumps(res, indent=1))
+    json.dump(res, open(os.path.join(a.dir, "traffic.json"), "w"), indent=1)
+    if a.emit:
+        json.dump(res, open("profiles/traffic_latest.json", "w"), indent=1)
+
+
+if __name__ == "__main__":
+    main()
