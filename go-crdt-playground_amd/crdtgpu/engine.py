@@ -46,6 +46,9 @@ class Engine:
     def reserve(self, max_docs: int, max_fold_slots: int = 0):
         check(self._lib.crdt_ctx_reserve(self._ctx, int(max_docs), int(max_fold_slots)), "crdt_ctx_reserve")
 
+    def set_max_doc_entries(self, n: int = 0xFFFFFFFF):
+        check(self._lib.crdt_ctx_set_max_doc_entries(self._ctx, int(n)), "crdt_ctx_set_max_doc_entries")
+
     def sync(self, stream=None):
         check(self._lib.crdt_ctx_sync(self._ctx, _stream(stream)), "crdt_ctx_sync")
 

@@ -12,7 +12,7 @@
 
 namespace crdt {
 hipError_t launch_join(const BatchView& dst, const BatchView& src, const OutView& out, const Work& wk,
-                       uint32_t block_grid, hipStream_t stream);
+                       uint32_t wave_grid, uint32_t block_grid, bool no_large, hipStream_t stream);
 hipError_t launch_fold(int mode, const BatchView& dst, const SrcView& sb, const OutView& out, const Scratch& scr,
                        const Work& wk, uint32_t block_grid, hipStream_t stream);
 hipError_t launch_vv_max(uint64_t* dst, const uint64_t* src, size_t n, hipStream_t stream);
@@ -63,6 +63,7 @@ struct crdt_ctx {
     DevBuf parts;
     DevBuf scratch;  // fold block path ping-pong: keys | actors | counters
     size_t scratch_slots = 0;
+    uint32_t max_doc_entries = 0xFFFFFFFFu;  // caller's promise (crdt_ctx_set_max_doc_entries)
     // staging for the *_batch host path
     DevBuf stage[24];
     hipStream_t stream = nullptr;
@@ -75,6 +76,7 @@ int hip_err(hipError_t e) { return e == hipSuccess ? CRDT_OK : CRDT_E_HIP; }
 int set_device(crdt_ctx* ctx) { return hip_err(hipSetDevice(ctx->device)); }
 
 uint32_t block_grid(const crdt_ctx* ctx) { return (uint32_t)ctx->n_cu * 2u; }
+uint32_t wave_grid(const crdt_ctx* ctx) { return (uint32_t)ctx->n_cu * 8u; }
 
 Work make_work(crdt_ctx* ctx) {
     Work w;
@@ -184,6 +186,12 @@ int crdt_ctx_reserve(crdt_ctx* ctx, uint32_t max_docs, uint64_t max_fold_slots) 
     return rc;
 }
 
+int crdt_ctx_set_max_doc_entries(crdt_ctx* ctx, uint32_t max_entries) {
+    if (!ctx) return CRDT_E_INVALID;
+    ctx->max_doc_entries = max_entries;
+    return CRDT_OK;
+}
+
 int crdt_ctx_sync(crdt_ctx* ctx, void* stream) {
     if (!ctx) return CRDT_E_INVALID;
     int rc = set_device(ctx);
@@ -197,6 +205,7 @@ int crdt_ctx_sync(crdt_ctx* ctx, void* stream) {
         if (hipMemset(ctx->ws.as<uint32_t>(16), 0, sizeof(uint32_t)) != hipSuccess) return CRDT_E_HIP;
         if (status & kErrActorRange) return CRDT_E_ACTOR_RANGE;
         if (status & kErrWorkspace) return CRDT_E_WORKSPACE;
+        if (status & kErrHint) return CRDT_E_INVALID;
     }
     return CRDT_OK;
 }
@@ -210,7 +219,8 @@ int crdt_awset_join_async(crdt_ctx* ctx, const crdt_awset_batch* dst, const crdt
     if (rc != CRDT_OK) return rc;
     hipStream_t s = (hipStream_t)stream;
     if (hipMemsetAsync(ctx->ws.p, 0, 16, s) != hipSuccess) return CRDT_E_HIP;
-    return hip_err(launch_join(view(dst), view(src), view(out), make_work(ctx), block_grid(ctx), s));
+    return hip_err(launch_join(view(dst), view(src), view(out), make_work(ctx), wave_grid(ctx), block_grid(ctx),
+                               ctx->max_doc_entries <= 64, s));
 }
 
 int crdt_awset_fold_async(crdt_ctx* ctx, int mode, const crdt_awset_batch* dst, const crdt_src_batch* srcs,

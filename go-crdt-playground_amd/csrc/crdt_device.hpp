@@ -17,6 +17,7 @@ constexpr int kWave = 64;
 // Device status bits (OR-ed into the context's status word).
 constexpr uint32_t kErrActorRange = 1u;
 constexpr uint32_t kErrWorkspace = 2u;  // fold scratch smaller than the output slots
+constexpr uint32_t kErrHint = 4u;       // a doc broke the crdt_ctx_set_max_doc_entries promise
 
 // Kernel-side view of an AWSet batch (same fields as crdt_awset_batch).
 struct BatchView {
@@ -110,13 +111,17 @@ __device__ __forceinline__ uint32_t popc(uint64_t m) { return (uint32_t)__popcll
 __device__ __forceinline__ uint64_t low_mask(uint32_t n) { return n >= 64 ? ~0ull : ((1ull << n) - 1ull); }
 
 // Number of elements of the sorted a[0..n) strictly less than key; n <= 2^LOG.
+// Branch-free: every probe reads (index 0 when the step is out of range), so a
+// wave runs LOG+1 LDS reads with no exec-mask juggling.
 template <int LOG>
 __device__ __forceinline__ uint32_t lower_bound_pow(const uint64_t* a, uint32_t n, uint64_t key) {
     uint32_t pos = 0;
 #pragma unroll
     for (int s = LOG; s >= 0; --s) {
-        uint32_t step = 1u << s;
-        if (pos + step <= n && a[pos + step - 1] < key) pos += step;
+        const uint32_t step = 1u << s;
+        const bool in = pos + step <= n;
+        const uint64_t v = a[in ? pos + step - 1 : 0u];
+        pos += (in && v < key) ? step : 0u;
     }
     return pos;
 }
@@ -138,6 +143,39 @@ __device__ __forceinline__ uint32_t lower_bound(const uint64_t* a, uint32_t n, u
 template <typename T>
 __device__ __forceinline__ T uniform(T v) {
     return (T)__builtin_amdgcn_readfirstlane((int)v);
+}
+
+// ---- buffer resources (T8): per-document descriptors built from wave-uniform
+// values.  A lane whose byte offset falls outside the descriptor reads 0 and
+// its store is dropped, so partially filled documents need no exec masking and
+// every memory op of a loop body can issue unconditionally.
+using rsrc_t = __amdgpu_buffer_rsrc_t;
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+constexpr uint32_t kOOB = 0x80000000u;  // byte offset past any descriptor
+
+__device__ __forceinline__ rsrc_t make_rsrc(const void* p, uint32_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ uint64_t ld64(rsrc_t r, uint32_t off) {
+    return __builtin_bit_cast(uint64_t, __builtin_amdgcn_raw_buffer_load_b64(r, (int)off, 0, 0));
+}
+__device__ __forceinline__ uint32_t ld32(rsrc_t r, uint32_t off) {
+    return (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(r, (int)off, 0, 0);
+}
+__device__ __forceinline__ void st64(uint64_t v, rsrc_t r, uint32_t off) {
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), r, (int)off, 0, 0);
+}
+__device__ __forceinline__ void st32(uint32_t v, rsrc_t r, uint32_t off) {
+    __builtin_amdgcn_raw_buffer_store_b32(v, r, (int)off, 0, 0);
+}
+
+// HasDot without branches (LDS read always issued); `call` says whether the
+// reference evaluates HasDot here, i.e. whether actor == R is its panic.
+__device__ __forceinline__ bool has_dot_bf(const uint64_t* vv, uint32_t R, uint32_t actor, uint64_t counter,
+                                           bool call, uint32_t& err) {
+    const uint64_t v = vv[actor < R ? actor : 0u];
+    err |= (call && actor == R) ? kErrActorRange : 0u;
+    return actor < R && v >= counter;
 }
 
 __device__ __forceinline__ void flag_error(uint32_t* status, uint32_t err) {

@@ -127,6 +127,11 @@ int crdt_ctx_create(int device, crdt_ctx** out);
 void crdt_ctx_destroy(crdt_ctx* ctx);
 /* Pre-size workspaces so that *_async calls never allocate (graph capture). */
 int crdt_ctx_reserve(crdt_ctx* ctx, uint32_t max_docs, uint64_t max_fold_slots);
+/* Promise that every doc of later joins holds <= max_entries live entries per
+ * side (0xFFFFFFFF = no promise, the default).  At <= 64 the large-document
+ * path is not launched; a doc that breaks the promise makes crdt_ctx_sync
+ * return CRDT_E_INVALID. */
+int crdt_ctx_set_max_doc_entries(crdt_ctx* ctx, uint32_t max_entries);
 /* Wait for `stream`, return (and clear) the first device-side error. */
 int crdt_ctx_sync(crdt_ctx* ctx, void* stream);
 const char* crdt_strerror(int code);
