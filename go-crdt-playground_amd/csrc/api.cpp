@@ -56,8 +56,8 @@ struct DevBuf {
 struct crdt_ctx {
     int device = 0;
     int n_cu = 256;
-    // [0,16): per-call counters {wl_count, wl_head, -, -} zeroed by every call;
-    // [16,20): status word, cleared by crdt_ctx_sync.
+    // [0,64): per-call counters {wl_count, wl_head, -, ..., chunk_ctr[8] at 32}
+    // zeroed by every call; [64,68): status word, cleared by crdt_ctx_sync.
     DevBuf ws;
     DevBuf worklist;
     DevBuf parts;
@@ -82,7 +82,8 @@ Work make_work(crdt_ctx* ctx) {
     Work w;
     w.wl_count = ctx->ws.as<uint32_t>(0);
     w.wl_head = ctx->ws.as<uint32_t>(4);
-    w.status = ctx->ws.as<uint32_t>(16);
+    w.status = ctx->ws.as<uint32_t>(64);
+    w.chunk_ctr = ctx->ws.as<uint32_t>(32);
     w.worklist = ctx->worklist.as<uint32_t>();
     return w;
 }
@@ -153,8 +154,8 @@ int crdt_ctx_create(int device, crdt_ctx** out) {
     int rc = set_device(ctx);
     hipDeviceProp_t prop;
     if (rc == CRDT_OK && hipGetDeviceProperties(&prop, device) == hipSuccess) ctx->n_cu = prop.multiProcessorCount;
-    if (rc == CRDT_OK) rc = ctx->ws.reserve(64);
-    if (rc == CRDT_OK) rc = hip_err(hipMemset(ctx->ws.p, 0, 64));
+    if (rc == CRDT_OK) rc = ctx->ws.reserve(128);
+    if (rc == CRDT_OK) rc = hip_err(hipMemset(ctx->ws.p, 0, 128));
     if (rc == CRDT_OK) rc = reserve_worklist(ctx, 1024);
     if (rc == CRDT_OK) rc = ctx->parts.reserve((size_t)kCtxParts * CRDT_MAX_R * sizeof(uint64_t));
     if (rc == CRDT_OK) rc = hip_err(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
@@ -199,10 +200,10 @@ int crdt_ctx_sync(crdt_ctx* ctx, void* stream) {
     hipStream_t s = (hipStream_t)stream;
     if (hipStreamSynchronize(s) != hipSuccess) return CRDT_E_HIP;
     uint32_t status = 0;
-    if (hipMemcpy(&status, ctx->ws.as<uint32_t>(16), sizeof(status), hipMemcpyDeviceToHost) != hipSuccess)
+    if (hipMemcpy(&status, ctx->ws.as<uint32_t>(64), sizeof(status), hipMemcpyDeviceToHost) != hipSuccess)
         return CRDT_E_HIP;
     if (status) {
-        if (hipMemset(ctx->ws.as<uint32_t>(16), 0, sizeof(uint32_t)) != hipSuccess) return CRDT_E_HIP;
+        if (hipMemset(ctx->ws.as<uint32_t>(64), 0, sizeof(uint32_t)) != hipSuccess) return CRDT_E_HIP;
         if (status & kErrActorRange) return CRDT_E_ACTOR_RANGE;
         if (status & kErrWorkspace) return CRDT_E_WORKSPACE;
         if (status & kErrHint) return CRDT_E_INVALID;
@@ -218,7 +219,7 @@ int crdt_awset_join_async(crdt_ctx* ctx, const crdt_awset_batch* dst, const crdt
     if (rc == CRDT_OK) rc = reserve_worklist(ctx, dst->n_docs);
     if (rc != CRDT_OK) return rc;
     hipStream_t s = (hipStream_t)stream;
-    if (hipMemsetAsync(ctx->ws.p, 0, 16, s) != hipSuccess) return CRDT_E_HIP;
+    if (hipMemsetAsync(ctx->ws.p, 0, 64, s) != hipSuccess) return CRDT_E_HIP;
     return hip_err(launch_join(view(dst), view(src), view(out), make_work(ctx), wave_grid(ctx), block_grid(ctx),
                                ctx->max_doc_entries <= 64, s));
 }
@@ -233,7 +234,7 @@ int crdt_awset_fold_async(crdt_ctx* ctx, int mode, const crdt_awset_batch* dst, 
     if (rc != CRDT_OK) return rc;
     if (ctx->scratch_slots == 0 && reserve_scratch(ctx, 1) != CRDT_OK) return CRDT_E_NOMEM;
     hipStream_t s = (hipStream_t)stream;
-    if (hipMemsetAsync(ctx->ws.p, 0, 16, s) != hipSuccess) return CRDT_E_HIP;
+    if (hipMemsetAsync(ctx->ws.p, 0, 64, s) != hipSuccess) return CRDT_E_HIP;
     const size_t slots = ctx->scratch_slots;
     Scratch scr{ctx->scratch.as<uint64_t>(0), ctx->scratch.as<uint32_t>(slots * 16), ctx->scratch.as<uint64_t>(slots * 8),
                 slots};

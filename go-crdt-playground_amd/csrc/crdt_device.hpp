@@ -68,6 +68,7 @@ struct Work {
     uint32_t* wl_count;    // number of docs pushed to the block-path worklist
     uint32_t* wl_head;     // dequeue head of the block path
     uint32_t* worklist;    // [n_docs]
+    uint32_t* chunk_ctr;   // [8] chunk dispenser shards of the wave path
 };
 
 __device__ __forceinline__ uint32_t live_count(const uint32_t* offsets, const uint32_t* counts, uint32_t d) {

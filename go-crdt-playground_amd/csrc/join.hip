@@ -17,28 +17,39 @@
 
 namespace crdt {
 
-// Per-doc metadata, fetched by lanes 0..3 with ONE vector load (in-order vmcnt,
-// so it can run ahead of the LDS traffic without forcing lgkmcnt(0) waits).
-// Unconditional: lanes >= 4 repeat lane 3's address, d is clamped.
+constexpr uint32_t kChunk = 64;          // documents per work chunk (one metadata vector)
+constexpr uint32_t kNone = 0xFFFFFFFFu;
+
 struct JoinMeta {
     uint32_t doff, soff, dn, sn;
 };
 
-__device__ __forceinline__ uint32_t meta_issue(const BatchView& dst, const BatchView& src, uint32_t d,
-                                               uint32_t lane) {
-    const uint32_t dd = d < dst.n_docs ? d : dst.n_docs - 1;
-    const uint32_t* p2 = dst.counts ? dst.counts + dd : dst.offsets + dd + 1;
-    const uint32_t* p3 = src.counts ? src.counts + dd : src.offsets + dd + 1;
-    const uint32_t* p = lane == 0 ? dst.offsets + dd : lane == 1 ? src.offsets + dd : lane == 2 ? p2 : p3;
-    return *p;
+// Metadata of the 64 documents of a chunk, lane i = document c*64 + i: one
+// unconditional vector load per field (indices clamped).
+struct MetaVec {
+    uint32_t doff, soff, dend, send;
+};
+
+__device__ __forceinline__ MetaVec meta_vec_issue(const BatchView& dst, const BatchView& src, uint32_t c,
+                                                  uint32_t lane) {
+    const uint32_t n = dst.n_docs;
+    const uint32_t d0 = (c == kNone ? 0u : c) * kChunk + lane;
+    const uint32_t dd = d0 < n ? d0 : n - 1;
+    MetaVec v;
+    v.doff = dst.offsets[dd];
+    v.soff = src.offsets[dd];
+    v.dend = dst.counts ? dst.counts[dd] : dst.offsets[dd + 1];
+    v.send = src.counts ? src.counts[dd] : src.offsets[dd + 1];
+    return v;
 }
 
-__device__ __forceinline__ JoinMeta meta_decode(const BatchView& dst, const BatchView& src, uint32_t v) {
+__device__ __forceinline__ JoinMeta meta_of(const BatchView& dst, const BatchView& src, const MetaVec& v,
+                                            uint32_t i) {
     JoinMeta m;
-    m.doff = (uint32_t)__builtin_amdgcn_readlane((int)v, 0);
-    m.soff = (uint32_t)__builtin_amdgcn_readlane((int)v, 1);
-    const uint32_t a = (uint32_t)__builtin_amdgcn_readlane((int)v, 2);
-    const uint32_t b = (uint32_t)__builtin_amdgcn_readlane((int)v, 3);
+    m.doff = (uint32_t)__builtin_amdgcn_readlane((int)v.doff, (int)i);
+    m.soff = (uint32_t)__builtin_amdgcn_readlane((int)v.soff, (int)i);
+    const uint32_t a = (uint32_t)__builtin_amdgcn_readlane((int)v.dend, (int)i);
+    const uint32_t b = (uint32_t)__builtin_amdgcn_readlane((int)v.send, (int)i);
     m.dn = dst.counts ? a : a - m.doff;
     m.sn = src.counts ? b : b - m.soff;
     return m;
@@ -50,7 +61,7 @@ struct JoinLanes {
     uint32_t da, sa;
 };
 
-// ld = false (document on the block path, or past the end): every lane reads 0.
+// ld = false (document on the block path, or none): every lane reads 0, no traffic.
 __device__ __forceinline__ void lanes_issue(JoinLanes& L, const BatchView& dst, const BatchView& src,
                                             const JoinMeta& m, uint32_t d, bool ld, uint32_t lane, uint32_t R) {
     const uint32_t dn = ld ? m.dn : 0u, sn = ld ? m.sn : 0u, rv = ld ? R : 0u;
@@ -66,105 +77,169 @@ __device__ __forceinline__ void lanes_issue(JoinLanes& L, const BatchView& dst, 
     L.vs = ld64(make_rsrc(src.vv + vo, rv * 8u), o8);
 }
 
-// Persistent waves, software-pipelined over the documents d = gw, gw + nw, ...:
-// metadata two documents ahead, entries one document ahead, so the loads of
-// the next document are in flight while this one is merged.  The loop body is
-// straight-line VMEM (buffer ops, no exec-masked branches) so the compiler's
-// vmcnt waits count exactly instead of draining to 0.
+// Chunk dispenser: 8 counters (one per blockIdx % 8 group, i.e. per XCD under
+// round-robin dispatch -- speed only), chunk = k * 8 + shard; an exhausted
+// shard falls through to the others.  Non-resident blocks simply get less work.
+__device__ __forceinline__ uint32_t grab_chunk(uint32_t* ctr, uint32_t shard, uint32_t n_chunks, uint32_t lane) {
+    for (uint32_t t = 0; t < 8; ++t) {
+        const uint32_t sh = (shard + t) & 7u;
+        uint32_t k = 0;
+        if (lane == 0) k = atomicAdd(ctr + sh, 1u);
+        k = (uint32_t)__builtin_amdgcn_readfirstlane((int)k);
+        const uint64_t c = (uint64_t)k * 8u + sh;
+        if (c < n_chunks) return (uint32_t)c;
+    }
+    return kNone;
+}
+
+struct ChunkState {
+    MetaVec cur, nxt;
+    uint32_t c, c2, i, nc;
+};
+
+template <int WAVES>
+struct JoinWaveSmem {
+    uint64_t dkey[WAVES][64];
+    uint64_t skey[WAVES][64];
+    uint64_t dvv[WAVES][64];
+    uint64_t svv[WAVES][64];
+};
+
+// Merge document d whose entries are in L (awset.go:107-161).
+template <int WAVES>
+__device__ __forceinline__ void join_doc(JoinWaveSmem<WAVES>& sm, uint32_t w, const JoinLanes& L, const JoinMeta& m,
+                                         uint32_t d, bool small, const OutView& out, uint32_t n_docs,
+                                         uint32_t end_off, uint32_t R, uint32_t lane, uint64_t lt, uint32_t& err) {
+    const uint32_t obase = m.doff + m.soff;
+    const uint32_t dnn = small ? m.dn : 0u, snn = small ? m.sn : 0u;
+    const bool dv = lane < dnn, sv = lane < snn;
+    sm.dvv[w][lane] = L.vd;
+    sm.svv[w][lane] = L.vs;
+    sm.dkey[w][lane] = L.dk;
+    sm.skey[w][lane] = L.sk;
+    wave_sync();
+    // # src keys < dk, # dst keys < sk
+    const uint32_t j = lower_bound_pow<6>(sm.skey[w], snn, L.dk);
+    const uint32_t i = lower_bound_pow<6>(sm.dkey[w], dnn, L.sk);
+    const bool dmatch = dv && j < snn && sm.skey[w][j & 63] == L.dk;
+    const bool smatch = sv && i < dnn && sm.dkey[w][i & 63] == L.sk;
+    // awset.go:145-159: a dst-only key survives unless src's clock covers it.
+    const bool dh = has_dot_bf(sm.svv[w], R, L.da, L.dc, dv && !dmatch, err);
+    // awset.go:130-140: a src-only key is added unless dst's clock covers it.
+    const bool sh = has_dot_bf(sm.dvv[w], R, L.sa, L.sc, sv && !smatch, err);
+    const bool dkeep = dv && (dmatch || !dh);
+    const bool skeep = sv && !smatch && !sh;
+    const uint64_t dm = ballot(dkeep), smk = ballot(skeep);
+    // awset.go:142: the src dot wins on a common key (lane j holds it).
+    const uint32_t ma = __shfl(L.sa, (int)(j & 63));
+    const uint64_t mc = __shfl(L.sc, (int)(j & 63));
+    const uint32_t dpos = popc(dm & lt) + popc(smk & low_mask(j));
+    const uint32_t spos = popc(smk & lt) + popc(dm & low_mask(i));
+    const uint32_t cap = dnn + snn;
+    const rsrc_t ok = make_rsrc(out.keys + obase, cap * 8u);
+    const rsrc_t oa = make_rsrc(out.actors + obase, cap * 4u);
+    const rsrc_t oc = make_rsrc(out.counters + obase, cap * 8u);
+    const uint32_t d8 = dkeep ? dpos * 8u : kOOB, d4 = dkeep ? dpos * 4u : kOOB;
+    const uint32_t s8 = skeep ? spos * 8u : kOOB, s4 = skeep ? spos * 4u : kOOB;
+    st64(L.dk, ok, d8);
+    st32(dmatch ? ma : L.da, oa, d4);
+    st64(dmatch ? mc : L.dc, oc, d8);
+    st64(L.sk, ok, s8);
+    st32(L.sa, oa, s4);
+    st64(L.sc, oc, s8);
+    // slot bounds (every doc), live count and VV (wave path only)
+    const bool last = d == n_docs - 1;
+    st32(lane == 0 ? obase : end_off, make_rsrc(out.offsets + d, last ? 8u : 4u), lane < 2 ? lane * 4u : kOOB);
+    st32(popc(dm) + popc(smk), make_rsrc(out.counts + d, small ? 4u : 0u), lane == 0 ? 0u : kOOB);
+    // awset.go:160 -> crdt-misc.go:43-55
+    st64(L.vd > L.vs ? L.vd : L.vs, make_rsrc(out.vv + (size_t)d * R, small ? R * 8u : 0u), lane * 8u);
+    wave_sync();
+}
+
+// Persistent waves over 64-document chunks.  Per document: the NEXT
+// document's entries are issued before this one is merged (ping-pong register
+// sets, no copies), so a wave always has one document's loads in flight.  The
+// loop body is straight-line buffer VMEM, so the compiler's vmcnt waits count
+// exactly instead of draining to 0; metadata comes from a per-chunk vector
+// (readlane), refreshed once per 64 documents.
 template <int WAVES>
 __global__ __launch_bounds__(WAVES * 64) void join_wave_kernel(BatchView dst, BatchView src, OutView out, Work wk,
                                                                uint32_t no_large) {
-    __shared__ uint64_t s_dkey[WAVES][64];
-    __shared__ uint64_t s_skey[WAVES][64];
-    __shared__ uint64_t s_dvv[WAVES][64];
-    __shared__ uint64_t s_svv[WAVES][64];
+    __shared__ JoinWaveSmem<WAVES> sm;
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t w = threadIdx.x >> 6;
     const uint32_t R = dst.R;
     const uint32_t n_docs = dst.n_docs;
-    const uint32_t nw = gridDim.x * WAVES;
+    const uint32_t n_chunks = (n_docs + kChunk - 1) / kChunk;
+    const uint32_t shard = blockIdx.x & 7u;
     const uint64_t lt = low_mask(lane);
     const uint32_t end_off = dst.offsets[n_docs] + src.offsets[n_docs];
     uint32_t err = 0;
 
-    uint32_t d = uniform(blockIdx.x * WAVES + w);
-    if (d >= n_docs) return;
-    JoinMeta m = meta_decode(dst, src, meta_issue(dst, src, d, lane));
-    uint32_t mv_next = meta_issue(dst, src, d + nw, lane);
-    JoinLanes cur;
+    ChunkState cs;
+    cs.c = grab_chunk(wk.chunk_ctr, shard, n_chunks, lane);
+    if (cs.c == kNone) return;
+    cs.cur = meta_vec_issue(dst, src, cs.c, lane);
+    cs.c2 = grab_chunk(wk.chunk_ctr, shard, n_chunks, lane);
+    cs.nxt = meta_vec_issue(dst, src, cs.c2, lane);
+    cs.i = 0;
+    cs.nc = min(kChunk, n_docs - cs.c * kChunk);
+
+    JoinMeta m = meta_of(dst, src, cs.cur, 0);
+    uint32_t d = cs.c * kChunk;
     bool small = m.dn <= 64 && m.sn <= 64;
-    lanes_issue(cur, dst, src, m, d, small, lane, R);
+    JoinLanes LA, LB;
+    lanes_issue(LA, dst, src, m, d, small, lane, R);
+
+    // advance to the next document (rolls the chunk state); false = none left
+    auto next = [&](JoinMeta& mn, uint32_t& dn) -> bool {
+        if (cs.i + 1 < cs.nc) {
+            ++cs.i;
+        } else {
+            if (cs.c2 == kNone) return false;
+            cs.c = cs.c2;
+            cs.cur = cs.nxt;
+            cs.i = 0;
+            cs.nc = min(kChunk, n_docs - cs.c * kChunk);
+            cs.c2 = grab_chunk(wk.chunk_ctr, shard, n_chunks, lane);
+            cs.nxt = meta_vec_issue(dst, src, cs.c2, lane);
+        }
+        mn = meta_of(dst, src, cs.cur, cs.i);
+        dn = cs.c * kChunk + cs.i;
+        return true;
+    };
+    auto push_large = [&](uint32_t dd) {
+        if (lane == 0) {
+            if (no_large)
+                atomicOr(wk.status, kErrHint);
+            else
+                wk.worklist[atomicAdd(wk.wl_count, 1u)] = dd;
+        }
+    };
 
     for (;;) {
-        const uint32_t dn = d + nw;
-        const bool more = dn < n_docs;
-        // stage 1: next document's metadata is back; issue its entries and the
-        // metadata after it.
-        const JoinMeta mn = meta_decode(dst, src, mv_next);
-        const bool small_n = more && mn.dn <= 64 && mn.sn <= 64;
-        const uint32_t mv_next2 = meta_issue(dst, src, dn + nw, lane);
-        JoinLanes nxt;
-        lanes_issue(nxt, dst, src, mn, dn, small_n, lane, R);
-
-        // stage 2: merge document d (awset.go:107-161).
-        const uint32_t obase = m.doff + m.soff;
-        const uint32_t dnn = small ? m.dn : 0u, snn = small ? m.sn : 0u;
-        const bool dv = lane < dnn, sv = lane < snn;
-        s_dvv[w][lane] = cur.vd;
-        s_svv[w][lane] = cur.vs;
-        s_dkey[w][lane] = cur.dk;
-        s_skey[w][lane] = cur.sk;
-        wave_sync();
-        // # src keys < dk, # dst keys < sk
-        const uint32_t j = lower_bound_pow<6>(s_skey[w], snn, cur.dk);
-        const uint32_t i = lower_bound_pow<6>(s_dkey[w], dnn, cur.sk);
-        const bool dmatch = dv && j < snn && s_skey[w][j & 63] == cur.dk;
-        const bool smatch = sv && i < dnn && s_dkey[w][i & 63] == cur.sk;
-        // awset.go:145-159: a dst-only key survives unless src's clock covers it.
-        const bool dh = has_dot_bf(s_svv[w], R, cur.da, cur.dc, dv && !dmatch, err);
-        // awset.go:130-140: a src-only key is added unless dst's clock covers it.
-        const bool sh = has_dot_bf(s_dvv[w], R, cur.sa, cur.sc, sv && !smatch, err);
-        const bool dkeep = dv && (dmatch || !dh);
-        const bool skeep = sv && !smatch && !sh;
-        const uint64_t dm = ballot(dkeep), sm = ballot(skeep);
-        // awset.go:142: the src dot wins on a common key (lane j holds it).
-        const uint32_t ma = __shfl(cur.sa, (int)(j & 63));
-        const uint64_t mc = __shfl(cur.sc, (int)(j & 63));
-        const uint32_t dpos = popc(dm & lt) + popc(sm & low_mask(j));
-        const uint32_t spos = popc(sm & lt) + popc(dm & low_mask(i));
-        const uint32_t cap = dnn + snn;
-        const rsrc_t ok = make_rsrc(out.keys + obase, cap * 8u);
-        const rsrc_t oa = make_rsrc(out.actors + obase, cap * 4u);
-        const rsrc_t oc = make_rsrc(out.counters + obase, cap * 8u);
-        const uint32_t d8 = dkeep ? dpos * 8u : kOOB, d4 = dkeep ? dpos * 4u : kOOB;
-        const uint32_t s8 = skeep ? spos * 8u : kOOB, s4 = skeep ? spos * 4u : kOOB;
-        st64(cur.dk, ok, d8);
-        st32(dmatch ? ma : cur.da, oa, d4);
-        st64(dmatch ? mc : cur.dc, oc, d8);
-        st64(cur.sk, ok, s8);
-        st32(cur.sa, oa, s4);
-        st64(cur.sc, oc, s8);
-        // slot bounds (every doc), live count and VV (wave path only)
-        const bool last = d == n_docs - 1;
-        st32(lane == 0 ? obase : end_off, make_rsrc(out.offsets + d, last ? 8u : 4u), lane < 2 ? lane * 4u : kOOB);
-        st32(popc(dm) + popc(sm), make_rsrc(out.counts + d, small ? 4u : 0u), lane == 0 ? 0u : kOOB);
-        // awset.go:160 -> crdt-misc.go:43-55
-        st64(cur.vd > cur.vs ? cur.vd : cur.vs, make_rsrc(out.vv + (size_t)d * R, small ? R * 8u : 0u), lane * 8u);
-        wave_sync();
-        if (!small) {
-            if (lane == 0) {
-                if (no_large)
-                    atomicOr(wk.status, kErrHint);
-                else
-                    wk.worklist[atomicAdd(wk.wl_count, 1u)] = d;
-            }
-        }
+        // A: issue next into LB, merge LA
+        JoinMeta mn;
+        uint32_t dn = 0;
+        bool more = next(mn, dn);
+        bool small_n = more && mn.dn <= 64 && mn.sn <= 64;
+        lanes_issue(LB, dst, src, mn, dn, small_n, lane, R);
+        join_doc<WAVES>(sm, w, LA, m, d, small, out, n_docs, end_off, R, lane, lt, err);
+        if (!small) push_large(d);
         if (!more) break;
-        d = dn;
         m = mn;
-        cur = nxt;
+        d = dn;
         small = small_n;
-        mv_next = mv_next2;
+        // B: issue next into LA, merge LB
+        more = next(mn, dn);
+        small_n = more && mn.dn <= 64 && mn.sn <= 64;
+        lanes_issue(LA, dst, src, mn, dn, small_n, lane, R);
+        join_doc<WAVES>(sm, w, LB, m, d, small, out, n_docs, end_off, R, lane, lt, err);
+        if (!small) push_large(d);
+        if (!more) break;
+        m = mn;
+        d = dn;
+        small = small_n;
     }
     flag_error(wk.status, err);
 }
@@ -212,7 +287,8 @@ constexpr int kBlockIPT = 4;
 hipError_t launch_join(const BatchView& dst, const BatchView& src, const OutView& out, const Work& wk,
                        uint32_t wave_grid, uint32_t block_grid, bool no_large, hipStream_t stream) {
     if (dst.n_docs == 0) return hipSuccess;
-    uint32_t grid = (dst.n_docs + kJoinWaves - 1) / kJoinWaves;
+    const uint32_t chunks = (dst.n_docs + kChunk - 1) / kChunk;
+    uint32_t grid = (chunks + kJoinWaves - 1) / kJoinWaves;
     if (grid > wave_grid) grid = wave_grid;
     hipLaunchKernelGGL((join_wave_kernel<kJoinWaves>), dim3(grid), dim3(kJoinWaves * 64), 0, stream, dst, src, out,
                        wk, (uint32_t)no_large);
