@@ -49,6 +49,9 @@ class Engine:
     def set_max_doc_entries(self, n: int = 0xFFFFFFFF):
         check(self._lib.crdt_ctx_set_max_doc_entries(self._ctx, int(n)), "crdt_ctx_set_max_doc_entries")
 
+    def set_option(self, name: str, value: int):
+        check(self._lib.crdt_ctx_set_option(self._ctx, name.encode(), int(value)), "crdt_ctx_set_option")
+
     def sync(self, stream=None):
         check(self._lib.crdt_ctx_sync(self._ctx, _stream(stream)), "crdt_ctx_sync")
 

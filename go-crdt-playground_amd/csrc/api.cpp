@@ -12,7 +12,7 @@
 
 namespace crdt {
 hipError_t launch_join(const BatchView& dst, const BatchView& src, const OutView& out, const Work& wk,
-                       uint32_t wave_grid, uint32_t block_grid, bool no_large, hipStream_t stream);
+                       uint32_t docs_per_wave, uint32_t block_grid, bool no_large, hipStream_t stream);
 hipError_t launch_fold(int mode, const BatchView& dst, const SrcView& sb, const OutView& out, const Scratch& scr,
                        const Work& wk, uint32_t block_grid, hipStream_t stream);
 hipError_t launch_vv_max(uint64_t* dst, const uint64_t* src, size_t n, hipStream_t stream);
@@ -64,6 +64,7 @@ struct crdt_ctx {
     DevBuf scratch;  // fold block path ping-pong: keys | actors | counters
     size_t scratch_slots = 0;
     uint32_t max_doc_entries = 0xFFFFFFFFu;  // caller's promise (crdt_ctx_set_max_doc_entries)
+    uint32_t join_docs_per_wave = 8;          // crdt_ctx_set_option("join_docs_per_wave")
     // staging for the *_batch host path
     DevBuf stage[24];
     hipStream_t stream = nullptr;
@@ -76,7 +77,6 @@ int hip_err(hipError_t e) { return e == hipSuccess ? CRDT_OK : CRDT_E_HIP; }
 int set_device(crdt_ctx* ctx) { return hip_err(hipSetDevice(ctx->device)); }
 
 uint32_t block_grid(const crdt_ctx* ctx) { return (uint32_t)ctx->n_cu * 2u; }
-uint32_t wave_grid(const crdt_ctx* ctx) { return (uint32_t)ctx->n_cu * 8u; }
 
 Work make_work(crdt_ctx* ctx) {
     Work w;
@@ -193,6 +193,16 @@ int crdt_ctx_set_max_doc_entries(crdt_ctx* ctx, uint32_t max_entries) {
     return CRDT_OK;
 }
 
+int crdt_ctx_set_option(crdt_ctx* ctx, const char* name, int64_t value) {
+    if (!ctx || !name) return CRDT_E_INVALID;
+    if (!strcmp(name, "join_docs_per_wave")) {
+        if (value != 1 && value != 2 && value != 4 && value != 8 && value != 16) return CRDT_E_INVALID;
+        ctx->join_docs_per_wave = (uint32_t)value;
+        return CRDT_OK;
+    }
+    return CRDT_E_INVALID;
+}
+
 int crdt_ctx_sync(crdt_ctx* ctx, void* stream) {
     if (!ctx) return CRDT_E_INVALID;
     int rc = set_device(ctx);
@@ -220,7 +230,7 @@ int crdt_awset_join_async(crdt_ctx* ctx, const crdt_awset_batch* dst, const crdt
     if (rc != CRDT_OK) return rc;
     hipStream_t s = (hipStream_t)stream;
     if (hipMemsetAsync(ctx->ws.p, 0, 64, s) != hipSuccess) return CRDT_E_HIP;
-    return hip_err(launch_join(view(dst), view(src), view(out), make_work(ctx), wave_grid(ctx), block_grid(ctx),
+    return hip_err(launch_join(view(dst), view(src), view(out), make_work(ctx), ctx->join_docs_per_wave, block_grid(ctx),
                                ctx->max_doc_entries <= 64, s));
 }
 

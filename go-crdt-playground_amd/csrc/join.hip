@@ -17,23 +17,20 @@
 
 namespace crdt {
 
-constexpr uint32_t kChunk = 64;          // documents per work chunk (one metadata vector)
-constexpr uint32_t kNone = 0xFFFFFFFFu;
-
 struct JoinMeta {
     uint32_t doff, soff, dn, sn;
 };
 
-// Metadata of the 64 documents of a chunk, lane i = document c*64 + i: one
+// Metadata of up to 64 documents, lane i = document first + i*stride: one
 // unconditional vector load per field (indices clamped).
 struct MetaVec {
     uint32_t doff, soff, dend, send;
 };
 
-__device__ __forceinline__ MetaVec meta_vec_issue(const BatchView& dst, const BatchView& src, uint32_t c,
-                                                  uint32_t lane) {
+__device__ __forceinline__ MetaVec meta_vec_issue(const BatchView& dst, const BatchView& src, uint32_t first,
+                                                  uint32_t stride, uint32_t lane) {
     const uint32_t n = dst.n_docs;
-    const uint32_t d0 = (c == kNone ? 0u : c) * kChunk + lane;
+    const uint32_t d0 = first + lane * stride;
     const uint32_t dd = d0 < n ? d0 : n - 1;
     MetaVec v;
     v.doff = dst.offsets[dd];
@@ -76,26 +73,6 @@ __device__ __forceinline__ void lanes_issue(JoinLanes& L, const BatchView& dst, 
     L.vd = ld64(make_rsrc(dst.vv + vo, rv * 8u), o8);
     L.vs = ld64(make_rsrc(src.vv + vo, rv * 8u), o8);
 }
-
-// Chunk dispenser: 8 counters (one per blockIdx % 8 group, i.e. per XCD under
-// round-robin dispatch -- speed only), chunk = k * 8 + shard; an exhausted
-// shard falls through to the others.  Non-resident blocks simply get less work.
-__device__ __forceinline__ uint32_t grab_chunk(uint32_t* ctr, uint32_t shard, uint32_t n_chunks, uint32_t lane) {
-    for (uint32_t t = 0; t < 8; ++t) {
-        const uint32_t sh = (shard + t) & 7u;
-        uint32_t k = 0;
-        if (lane == 0) k = atomicAdd(ctr + sh, 1u);
-        k = (uint32_t)__builtin_amdgcn_readfirstlane((int)k);
-        const uint64_t c = (uint64_t)k * 8u + sh;
-        if (c < n_chunks) return (uint32_t)c;
-    }
-    return kNone;
-}
-
-struct ChunkState {
-    MetaVec cur, nxt;
-    uint32_t c, c2, i, nc;
-};
 
 template <int WAVES>
 struct JoinWaveSmem {
@@ -156,13 +133,14 @@ __device__ __forceinline__ void join_doc(JoinWaveSmem<WAVES>& sm, uint32_t w, co
     wave_sync();
 }
 
-// Persistent waves over 64-document chunks.  Per document: the NEXT
-// document's entries are issued before this one is merged (ping-pong register
-// sets, no copies), so a wave always has one document's loads in flight.  The
-// loop body is straight-line buffer VMEM, so the compiler's vmcnt waits count
-// exactly instead of draining to 0; metadata comes from a per-chunk vector
-// (readlane), refreshed once per 64 documents.
-template <int WAVES>
+// A block covers the contiguous documents [blockIdx*WAVES*K, +WAVES*K); wave w
+// takes documents base + w + k*WAVES, k < K, so the documents in flight across
+// the GPU form one contiguous window (the dispatcher runs blocks roughly in
+// order).  Per wave: one metadata vector load for its K documents, then a
+// ping-pong pipeline -- the next document's entries are issued before this
+// one is merged.  The body is straight-line buffer VMEM, so the compiler's
+// vmcnt waits count exactly and the prefetch stays in flight.
+template <int WAVES, int K>
 __global__ __launch_bounds__(WAVES * 64) void join_wave_kernel(BatchView dst, BatchView src, OutView out, Work wk,
                                                                uint32_t no_large) {
     __shared__ JoinWaveSmem<WAVES> sm;
@@ -170,44 +148,15 @@ __global__ __launch_bounds__(WAVES * 64) void join_wave_kernel(BatchView dst, Ba
     const uint32_t w = threadIdx.x >> 6;
     const uint32_t R = dst.R;
     const uint32_t n_docs = dst.n_docs;
-    const uint32_t n_chunks = (n_docs + kChunk - 1) / kChunk;
-    const uint32_t shard = blockIdx.x & 7u;
     const uint64_t lt = low_mask(lane);
     const uint32_t end_off = dst.offsets[n_docs] + src.offsets[n_docs];
     uint32_t err = 0;
 
-    ChunkState cs;
-    cs.c = grab_chunk(wk.chunk_ctr, shard, n_chunks, lane);
-    if (cs.c == kNone) return;
-    cs.cur = meta_vec_issue(dst, src, cs.c, lane);
-    cs.c2 = grab_chunk(wk.chunk_ctr, shard, n_chunks, lane);
-    cs.nxt = meta_vec_issue(dst, src, cs.c2, lane);
-    cs.i = 0;
-    cs.nc = min(kChunk, n_docs - cs.c * kChunk);
+    const uint32_t first = uniform(blockIdx.x * (WAVES * K) + w);
+    if (first >= n_docs) return;
+    const uint32_t cnt = min((uint32_t)K, (n_docs - first + WAVES - 1) / WAVES);
+    const MetaVec mv = meta_vec_issue(dst, src, first, WAVES, lane);
 
-    JoinMeta m = meta_of(dst, src, cs.cur, 0);
-    uint32_t d = cs.c * kChunk;
-    bool small = m.dn <= 64 && m.sn <= 64;
-    JoinLanes LA, LB;
-    lanes_issue(LA, dst, src, m, d, small, lane, R);
-
-    // advance to the next document (rolls the chunk state); false = none left
-    auto next = [&](JoinMeta& mn, uint32_t& dn) -> bool {
-        if (cs.i + 1 < cs.nc) {
-            ++cs.i;
-        } else {
-            if (cs.c2 == kNone) return false;
-            cs.c = cs.c2;
-            cs.cur = cs.nxt;
-            cs.i = 0;
-            cs.nc = min(kChunk, n_docs - cs.c * kChunk);
-            cs.c2 = grab_chunk(wk.chunk_ctr, shard, n_chunks, lane);
-            cs.nxt = meta_vec_issue(dst, src, cs.c2, lane);
-        }
-        mn = meta_of(dst, src, cs.cur, cs.i);
-        dn = cs.c * kChunk + cs.i;
-        return true;
-    };
     auto push_large = [&](uint32_t dd) {
         if (lane == 0) {
             if (no_large)
@@ -217,26 +166,36 @@ __global__ __launch_bounds__(WAVES * 64) void join_wave_kernel(BatchView dst, Ba
         }
     };
 
-    for (;;) {
-        // A: issue next into LB, merge LA
-        JoinMeta mn;
-        uint32_t dn = 0;
-        bool more = next(mn, dn);
+    JoinMeta m = meta_of(dst, src, mv, 0);
+    uint32_t d = first;
+    bool small = m.dn <= 64 && m.sn <= 64;
+    JoinLanes LA, LB;
+    lanes_issue(LA, dst, src, m, d, small, lane, R);
+#pragma unroll 1
+    for (uint32_t k = 0;;) {
+        // A: issue k+1 into LB, merge LA
+        bool more = k + 1 < cnt;
+        JoinMeta mn = meta_of(dst, src, mv, more ? k + 1 : 0);
+        uint32_t dn = d + WAVES;
         bool small_n = more && mn.dn <= 64 && mn.sn <= 64;
         lanes_issue(LB, dst, src, mn, dn, small_n, lane, R);
         join_doc<WAVES>(sm, w, LA, m, d, small, out, n_docs, end_off, R, lane, lt, err);
         if (!small) push_large(d);
         if (!more) break;
+        ++k;
         m = mn;
         d = dn;
         small = small_n;
-        // B: issue next into LA, merge LB
-        more = next(mn, dn);
+        // B: issue k+1 into LA, merge LB
+        more = k + 1 < cnt;
+        mn = meta_of(dst, src, mv, more ? k + 1 : 0);
+        dn = d + WAVES;
         small_n = more && mn.dn <= 64 && mn.sn <= 64;
         lanes_issue(LA, dst, src, mn, dn, small_n, lane, R);
         join_doc<WAVES>(sm, w, LB, m, d, small, out, n_docs, end_off, R, lane, lt, err);
         if (!small) push_large(d);
         if (!more) break;
+        ++k;
         m = mn;
         d = dn;
         small = small_n;
@@ -281,17 +240,28 @@ constexpr int kJoinWaves = 4;
 constexpr int kBlockNT = 256;
 constexpr int kBlockIPT = 4;
 
-// wave_grid: persistent blocks of the wave path (a few per CU); no_large: the
+// docs_per_wave: K of join_wave_kernel (1, 2, 4, 8 or 16); no_large: the
 // caller promised every doc has <= 64 entries per side, so the block path is
 // not launched (a larger doc then raises CRDT_E_INVALID).
-hipError_t launch_join(const BatchView& dst, const BatchView& src, const OutView& out, const Work& wk,
-                       uint32_t wave_grid, uint32_t block_grid, bool no_large, hipStream_t stream) {
-    if (dst.n_docs == 0) return hipSuccess;
-    const uint32_t chunks = (dst.n_docs + kChunk - 1) / kChunk;
-    uint32_t grid = (chunks + kJoinWaves - 1) / kJoinWaves;
-    if (grid > wave_grid) grid = wave_grid;
-    hipLaunchKernelGGL((join_wave_kernel<kJoinWaves>), dim3(grid), dim3(kJoinWaves * 64), 0, stream, dst, src, out,
+template <int K>
+static void launch_wave(const BatchView& dst, const BatchView& src, const OutView& out, const Work& wk, bool no_large,
+                        hipStream_t stream) {
+    const uint32_t per_block = kJoinWaves * K;
+    const uint32_t grid = (dst.n_docs + per_block - 1) / per_block;
+    hipLaunchKernelGGL((join_wave_kernel<kJoinWaves, K>), dim3(grid), dim3(kJoinWaves * 64), 0, stream, dst, src, out,
                        wk, (uint32_t)no_large);
+}
+
+hipError_t launch_join(const BatchView& dst, const BatchView& src, const OutView& out, const Work& wk,
+                       uint32_t docs_per_wave, uint32_t block_grid, bool no_large, hipStream_t stream) {
+    if (dst.n_docs == 0) return hipSuccess;
+    switch (docs_per_wave) {
+        case 1: launch_wave<1>(dst, src, out, wk, no_large, stream); break;
+        case 2: launch_wave<2>(dst, src, out, wk, no_large, stream); break;
+        case 4: launch_wave<4>(dst, src, out, wk, no_large, stream); break;
+        case 16: launch_wave<16>(dst, src, out, wk, no_large, stream); break;
+        default: launch_wave<8>(dst, src, out, wk, no_large, stream); break;
+    }
     hipError_t e = hipGetLastError();
     if (e != hipSuccess || no_large) return e;
     hipLaunchKernelGGL((join_block_kernel<kBlockNT, kBlockIPT>), dim3(block_grid), dim3(kBlockNT), 0, stream, dst,
