@@ -12,7 +12,8 @@
 
 namespace crdt {
 hipError_t launch_join(const BatchView& dst, const BatchView& src, const OutView& out, const Work& wk,
-                       uint32_t docs_per_wave, uint32_t block_grid, bool no_large, hipStream_t stream);
+                       uint32_t docs_per_wave, bool nt_stores, uint32_t block_grid, bool no_large,
+                       hipStream_t stream);
 hipError_t launch_fold(int mode, const BatchView& dst, const SrcView& sb, const OutView& out, const Scratch& scr,
                        const Work& wk, uint32_t block_grid, hipStream_t stream);
 hipError_t launch_vv_max(uint64_t* dst, const uint64_t* src, size_t n, hipStream_t stream);
@@ -65,6 +66,7 @@ struct crdt_ctx {
     size_t scratch_slots = 0;
     uint32_t max_doc_entries = 0xFFFFFFFFu;  // caller's promise (crdt_ctx_set_max_doc_entries)
     uint32_t join_docs_per_wave = 8;          // crdt_ctx_set_option("join_docs_per_wave")
+    bool join_nt_stores = true;               // crdt_ctx_set_option("join_nt_stores")
     // staging for the *_batch host path
     DevBuf stage[24];
     hipStream_t stream = nullptr;
@@ -200,6 +202,10 @@ int crdt_ctx_set_option(crdt_ctx* ctx, const char* name, int64_t value) {
         ctx->join_docs_per_wave = (uint32_t)value;
         return CRDT_OK;
     }
+    if (!strcmp(name, "join_nt_stores")) {
+        ctx->join_nt_stores = value != 0;
+        return CRDT_OK;
+    }
     return CRDT_E_INVALID;
 }
 
@@ -230,7 +236,8 @@ int crdt_awset_join_async(crdt_ctx* ctx, const crdt_awset_batch* dst, const crdt
     if (rc != CRDT_OK) return rc;
     hipStream_t s = (hipStream_t)stream;
     if (hipMemsetAsync(ctx->ws.p, 0, 64, s) != hipSuccess) return CRDT_E_HIP;
-    return hip_err(launch_join(view(dst), view(src), view(out), make_work(ctx), ctx->join_docs_per_wave, block_grid(ctx),
+    return hip_err(launch_join(view(dst), view(src), view(out), make_work(ctx), ctx->join_docs_per_wave, ctx->join_nt_stores,
+                               block_grid(ctx),
                                ctx->max_doc_entries <= 64, s));
 }
 

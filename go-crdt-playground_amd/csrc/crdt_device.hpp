@@ -163,11 +163,16 @@ __device__ __forceinline__ uint64_t ld64(rsrc_t r, uint32_t off) {
 __device__ __forceinline__ uint32_t ld32(rsrc_t r, uint32_t off) {
     return (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(r, (int)off, 0, 0);
 }
+// AUX = cache policy bits of the buffer instruction (gfx950: 2 = nt,
+// non-temporal: streaming output that no kernel of this launch re-reads).
+constexpr int kAuxNT = 2;
+template <int AUX = 0>
 __device__ __forceinline__ void st64(uint64_t v, rsrc_t r, uint32_t off) {
-    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), r, (int)off, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), r, (int)off, 0, AUX);
 }
+template <int AUX = 0>
 __device__ __forceinline__ void st32(uint32_t v, rsrc_t r, uint32_t off) {
-    __builtin_amdgcn_raw_buffer_store_b32(v, r, (int)off, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b32(v, r, (int)off, 0, AUX);
 }
 
 // HasDot without branches (LDS read always issued); `call` says whether the

@@ -82,8 +82,9 @@ struct JoinWaveSmem {
     uint64_t svv[WAVES][64];
 };
 
-// Merge document d whose entries are in L (awset.go:107-161).
-template <int WAVES>
+// Merge document d whose entries are in L (awset.go:107-161).  AUX: cache
+// policy of the entry stores (0 plain, kAuxNT non-temporal).
+template <int WAVES, int AUX>
 __device__ __forceinline__ void join_doc(JoinWaveSmem<WAVES>& sm, uint32_t w, const JoinLanes& L, const JoinMeta& m,
                                          uint32_t d, bool small, const OutView& out, uint32_t n_docs,
                                          uint32_t end_off, uint32_t R, uint32_t lane, uint64_t lt, uint32_t& err) {
@@ -118,12 +119,12 @@ __device__ __forceinline__ void join_doc(JoinWaveSmem<WAVES>& sm, uint32_t w, co
     const rsrc_t oc = make_rsrc(out.counters + obase, cap * 8u);
     const uint32_t d8 = dkeep ? dpos * 8u : kOOB, d4 = dkeep ? dpos * 4u : kOOB;
     const uint32_t s8 = skeep ? spos * 8u : kOOB, s4 = skeep ? spos * 4u : kOOB;
-    st64(L.dk, ok, d8);
-    st32(dmatch ? ma : L.da, oa, d4);
-    st64(dmatch ? mc : L.dc, oc, d8);
-    st64(L.sk, ok, s8);
-    st32(L.sa, oa, s4);
-    st64(L.sc, oc, s8);
+    st64<AUX>(L.dk, ok, d8);
+    st32<AUX>(dmatch ? ma : L.da, oa, d4);
+    st64<AUX>(dmatch ? mc : L.dc, oc, d8);
+    st64<AUX>(L.sk, ok, s8);
+    st32<AUX>(L.sa, oa, s4);
+    st64<AUX>(L.sc, oc, s8);
     // slot bounds (every doc), live count and VV (wave path only)
     const bool last = d == n_docs - 1;
     st32(lane == 0 ? obase : end_off, make_rsrc(out.offsets + d, last ? 8u : 4u), lane < 2 ? lane * 4u : kOOB);
@@ -140,7 +141,7 @@ __device__ __forceinline__ void join_doc(JoinWaveSmem<WAVES>& sm, uint32_t w, co
 // ping-pong pipeline -- the next document's entries are issued before this
 // one is merged.  The body is straight-line buffer VMEM, so the compiler's
 // vmcnt waits count exactly and the prefetch stays in flight.
-template <int WAVES, int K>
+template <int WAVES, int K, int AUX>
 __global__ __launch_bounds__(WAVES * 64) void join_wave_kernel(BatchView dst, BatchView src, OutView out, Work wk,
                                                                uint32_t no_large) {
     __shared__ JoinWaveSmem<WAVES> sm;
@@ -179,7 +180,7 @@ __global__ __launch_bounds__(WAVES * 64) void join_wave_kernel(BatchView dst, Ba
         uint32_t dn = d + WAVES;
         bool small_n = more && mn.dn <= 64 && mn.sn <= 64;
         lanes_issue(LB, dst, src, mn, dn, small_n, lane, R);
-        join_doc<WAVES>(sm, w, LA, m, d, small, out, n_docs, end_off, R, lane, lt, err);
+        join_doc<WAVES, AUX>(sm, w, LA, m, d, small, out, n_docs, end_off, R, lane, lt, err);
         if (!small) push_large(d);
         if (!more) break;
         ++k;
@@ -192,7 +193,7 @@ __global__ __launch_bounds__(WAVES * 64) void join_wave_kernel(BatchView dst, Ba
         dn = d + WAVES;
         small_n = more && mn.dn <= 64 && mn.sn <= 64;
         lanes_issue(LA, dst, src, mn, dn, small_n, lane, R);
-        join_doc<WAVES>(sm, w, LB, m, d, small, out, n_docs, end_off, R, lane, lt, err);
+        join_doc<WAVES, AUX>(sm, w, LB, m, d, small, out, n_docs, end_off, R, lane, lt, err);
         if (!small) push_large(d);
         if (!more) break;
         ++k;
@@ -240,28 +241,39 @@ constexpr int kJoinWaves = 4;
 constexpr int kBlockNT = 256;
 constexpr int kBlockIPT = 4;
 
-// docs_per_wave: K of join_wave_kernel (1, 2, 4, 8 or 16); no_large: the
-// caller promised every doc has <= 64 entries per side, so the block path is
-// not launched (a larger doc then raises CRDT_E_INVALID).
-template <int K>
+template <int K, int AUX>
 static void launch_wave(const BatchView& dst, const BatchView& src, const OutView& out, const Work& wk, bool no_large,
                         hipStream_t stream) {
     const uint32_t per_block = kJoinWaves * K;
     const uint32_t grid = (dst.n_docs + per_block - 1) / per_block;
-    hipLaunchKernelGGL((join_wave_kernel<kJoinWaves, K>), dim3(grid), dim3(kJoinWaves * 64), 0, stream, dst, src, out,
-                       wk, (uint32_t)no_large);
+    hipLaunchKernelGGL((join_wave_kernel<kJoinWaves, K, AUX>), dim3(grid), dim3(kJoinWaves * 64), 0, stream, dst, src,
+                       out, wk, (uint32_t)no_large);
 }
 
-hipError_t launch_join(const BatchView& dst, const BatchView& src, const OutView& out, const Work& wk,
-                       uint32_t docs_per_wave, uint32_t block_grid, bool no_large, hipStream_t stream) {
-    if (dst.n_docs == 0) return hipSuccess;
-    switch (docs_per_wave) {
-        case 1: launch_wave<1>(dst, src, out, wk, no_large, stream); break;
-        case 2: launch_wave<2>(dst, src, out, wk, no_large, stream); break;
-        case 4: launch_wave<4>(dst, src, out, wk, no_large, stream); break;
-        case 16: launch_wave<16>(dst, src, out, wk, no_large, stream); break;
-        default: launch_wave<8>(dst, src, out, wk, no_large, stream); break;
+template <int AUX>
+static void launch_wave_k(uint32_t k, const BatchView& dst, const BatchView& src, const OutView& out, const Work& wk,
+                          bool no_large, hipStream_t stream) {
+    switch (k) {
+        case 1: launch_wave<1, AUX>(dst, src, out, wk, no_large, stream); break;
+        case 2: launch_wave<2, AUX>(dst, src, out, wk, no_large, stream); break;
+        case 4: launch_wave<4, AUX>(dst, src, out, wk, no_large, stream); break;
+        case 16: launch_wave<16, AUX>(dst, src, out, wk, no_large, stream); break;
+        default: launch_wave<8, AUX>(dst, src, out, wk, no_large, stream); break;
     }
+}
+
+// docs_per_wave: K of join_wave_kernel (1, 2, 4, 8 or 16); nt_stores: write the
+// output with non-temporal stores; no_large: the caller promised every doc has
+// <= 64 entries per side, so the block path is not launched (a larger doc then
+// raises CRDT_E_INVALID).
+hipError_t launch_join(const BatchView& dst, const BatchView& src, const OutView& out, const Work& wk,
+                       uint32_t docs_per_wave, bool nt_stores, uint32_t block_grid, bool no_large,
+                       hipStream_t stream) {
+    if (dst.n_docs == 0) return hipSuccess;
+    if (nt_stores)
+        launch_wave_k<kAuxNT>(docs_per_wave, dst, src, out, wk, no_large, stream);
+    else
+        launch_wave_k<0>(docs_per_wave, dst, src, out, wk, no_large, stream);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess || no_large) return e;
     hipLaunchKernelGGL((join_block_kernel<kBlockNT, kBlockIPT>), dim3(block_grid), dim3(kBlockNT), 0, stream, dst,

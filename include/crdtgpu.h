@@ -133,7 +133,8 @@ int crdt_ctx_reserve(crdt_ctx* ctx, uint32_t max_docs, uint64_t max_fold_slots);
  * return CRDT_E_INVALID. */
 int crdt_ctx_set_max_doc_entries(crdt_ctx* ctx, uint32_t max_entries);
 /* Tuning knobs (performance only, never results):
- *   "join_docs_per_wave"  1|2|4|8|16  documents one wavefront pipelines (default 8) */
+ *   "join_docs_per_wave"  1|2|4|8|16  documents one wavefront pipelines (default 8)
+ *   "join_nt_stores"      0|1         non-temporal output stores (default 1) */
 int crdt_ctx_set_option(crdt_ctx* ctx, const char* name, int64_t value);
 /* Wait for `stream`, return (and clear) the first device-side error. */
 int crdt_ctx_sync(crdt_ctx* ctx, void* stream);
