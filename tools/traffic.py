@@ -41,24 +41,27 @@ def main():
     ap.add_argument("--docs", type=int, default=1 << 20)
     ap.add_argument("--emit", action="store_true")
     a = ap.parse_args()
-    out = {}
+    out, calib = {}, {}
     for sub in sorted(os.listdir(a.dir)):
         p = os.path.join(a.dir, sub)
         if not os.path.isdir(p):
             continue
+        dst = calib if sub.startswith("calib") else out
         for k, cs in load(p).items():
             for c, v in cs.items():
-                out.setdefault(short(k), {})[c] = sum(v) / len(v)
+                dst.setdefault(short(k), {})[c] = sum(v) / len(v)
     for k in sorted(out):
         print(k)
         for c, v in sorted(out[k].items()):
             print("   %-24s %.6g" % (c, v))
-    cal = out.get("vv_max_kernel", {})
+    cal = calib.get("vv_max_kernel", {})
+    print("calibration (vv_max_kernel, 1 GiB read / 512 MiB written per launch):", cal)
     N = 64 << 20
     fcorr = (16 * N) / (cal["FETCH_SIZE"] * 1024) if cal.get("FETCH_SIZE") else None
     wcorr = (8 * N) / (cal["WRITE_SIZE"] * 1024) if cal.get("WRITE_SIZE") else None
-    j = next((v for k, v in out.items() if k.startswith("join_wave_kernel")), {})
-    res = {"docs": a.docs, "kernel": "join_wave_kernel<4>", "fetch_correction": fcorr, "write_correction": wcorr}
+    jk = next((k for k in out if k.startswith("join_wave_kernel")), "")
+    j = out.get(jk, {})
+    res = {"docs": a.docs, "kernel": jk, "fetch_correction": fcorr, "write_correction": wcorr}
     if j.get("FETCH_SIZE") is not None and j.get("WRITE_SIZE") is not None:
         rd = j["FETCH_SIZE"] * 1024 * (fcorr or 1.0)
         wr = j["WRITE_SIZE"] * 1024 * (wcorr or 1.0)
