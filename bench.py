@@ -28,17 +28,6 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level table)
 
 
-def u64_max_allreduce(dist, t):
-    """all_reduce(MAX) of u64 values held in an int64 tensor: flip the sign bit so
-    signed order equals unsigned order, reduce, flip back (exact for all u64)."""
-    import torch
-
-    flip = torch.tensor(-(1 << 63), dtype=torch.int64, device=t.device)
-    x = t ^ flip
-    dist.all_reduce(x, op=dist.ReduceOp.MAX)
-    return x ^ flip
-
-
 def cpu_baseline(A, B, n_sample, budget_s):
     """Time the C oracle (single thread, the 'port' baseline) on the first
     n_sample docs of this rank's batch, both directions, repeated for ~budget_s."""
@@ -91,6 +80,7 @@ def main():
     import crdtgpu
     from crdtgpu.batch import OutBuffers
     from crdtgpu import workloads
+    from crdtgpu.dist import u64_max_allreduce
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
