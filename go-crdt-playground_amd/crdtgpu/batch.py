@@ -213,5 +213,24 @@ class SrcBatch:
         return int(_np(dst.offsets, U32)[-1]) + int(eo[-1])
 
 
+class SrcBuffers(SrcBatch):
+    """Device (torch) or host (numpy) storage for n_srcs sources of fixed
+    entry / tombstone slot counts (what the workload generators fill)."""
+
+    def __init__(self, R, n_docs, n_srcs, entry_slots, tomb_slots, device=None):
+        if device is None:
+            z = lambda n, dt: np.zeros(max(n, 1), dtype=dt)  # noqa: E731
+            i32, i64 = U32, U64
+        else:
+            import torch
+
+            z = lambda n, dt: torch.zeros(max(n, 1), dtype=dt, device=device)  # noqa: E731
+            i32, i64 = torch.int32, torch.int64
+        super().__init__(R, z(n_docs + 1, i32)[: n_docs + 1], z(n_srcs, i32)[:n_srcs], z(n_srcs * R, i64),
+                         z(n_srcs + 1, i32)[: n_srcs + 1], z(entry_slots, i64), z(entry_slots, i32),
+                         z(entry_slots, i64), z(n_srcs + 1, i32)[: n_srcs + 1], z(tomb_slots, i64),
+                         z(tomb_slots, i32), z(tomb_slots, i64))
+
+
 def c_ref(x):
     return ctypes.byref(x)

@@ -79,6 +79,11 @@ class Engine:
         check(self._lib.crdt_gen_pair_async(self._ctx, int(seed), int(n_docs), ctypes.byref(ca), ctypes.byref(cb),
                                             _stream(stream)), "crdt_gen_pair_async")
 
+    def gen_delta_async(self, seed: int, n_docs: int, R: int, M: int, dst: OutBuffers, srcs: SrcBatch, stream=None):
+        cd, cs = dst.c(), srcs.c()
+        check(self._lib.crdt_gen_delta_async(self._ctx, int(seed), int(n_docs), int(R), int(M), ctypes.byref(cd),
+                                             ctypes.byref(cs), _stream(stream)), "crdt_gen_delta_async")
+
     # -- host buffers, synchronous ----------------------------------------
     def join(self, dst: AWSetBatch, src: AWSetBatch) -> OutBuffers:
         dst, src = dst.numpy(), src.numpy()

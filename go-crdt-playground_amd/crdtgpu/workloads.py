@@ -64,6 +64,51 @@ def pair_docs(seed: int, docs):
     return A, B
 
 
+def _H(seed, d, tag, i):
+    return int(splitmix64(np.uint64((seed ^ (d << 20) ^ (tag << 12) ^ i) & M64)))
+
+
+def _subset256(h, k):
+    mul, add = (h & 0xFF) | 1, (h >> 8) & 0xFF
+    return [u for u in range(256) if ((mul * u + add) & 255) < k]
+
+
+def delta_docs(seed: int, docs, R: int = 16, M: int = 10):
+    """Host copy of the "delta" workload (csrc/gen.hip) for doc ids `docs`:
+    (dst docs [(entries, vv)], per-doc sources [(actor, vv, entries, tombstones)])."""
+    dsts, srcs = [], []
+    for d in docs:
+        first = _H(seed, d, 1, 0) % 100 == 0
+        astar = _H(seed, d, 1, 1) % R
+        vv0 = [0 if (first and r == astar) else 64 + _H(seed, d, 3, r) % 32 for r in range(R)]
+        ents = []
+        for u in _subset256(_H(seed, d, 0, 0), 64):
+            hu = _H(seed, d, 2, u)
+            a = hu % R
+            if first and a == astar:
+                a = (a + 1) % R
+            ents.append(((d << 8) | u, a, 1 + (hu >> 8) % 64))
+        dsts.append((ents, vv0))
+        chain = []
+        for j in range(M):
+            aj = astar if (first and j == 0) else _H(seed, d, 4, j) % R
+            svv = [vv0[r] + 1 + _H(seed, d, 5, j * R + r) % 16 for r in range(R)]
+            e = []
+            for u in _subset256(_H(seed, d, 6, j), 8):
+                he = _H(seed, d, 7, j * 256 + u)
+                a = (he >> 2) % R if (he & 3) == 0 else aj
+                v0, sv = vv0[a], svv[a]
+                c = 1 + (he >> 16) % (v0 if v0 > 0 else 1) if ((he >> 8) & 1) == 0 else v0 + 1 + (he >> 16) % (sv - v0)
+                e.append(((d << 8) | u, a, c))
+            t = []
+            for u in _subset256(_H(seed, d, 8, j), 2):
+                back = _H(seed, d, 9, j * 256 + u) % 8
+                t.append(((d << 8) | u, aj, svv[aj] - back if svv[aj] > back else 1))
+            chain.append((aj, svv, e, t))
+        srcs.append(chain)
+    return dsts, srcs
+
+
 def join_bytes(n_dst, n_src, n_out, R) -> int:
     """Σ over docs of 20(n_dst + n_src + n_out) + 24R + 12."""
     n_dst, n_src, n_out = (np.asarray(x, dtype=np.int64) for x in (n_dst, n_src, n_out))

@@ -20,6 +20,21 @@ hipError_t launch_vv_max(uint64_t* dst, const uint64_t* src, size_t n, hipStream
 hipError_t launch_context(const uint64_t* vv, uint32_t n_docs, uint32_t R, uint64_t* part, uint32_t n_part,
                           uint64_t* out, hipStream_t stream);
 hipError_t launch_gen_pair(uint64_t seed, uint32_t n_docs, const OutView& A, const OutView& B, hipStream_t stream);
+struct SrcOutView {
+    uint32_t* doc_srcs;
+    uint32_t* src_actor;
+    uint64_t* vv;
+    uint32_t* entry_off;
+    uint64_t* keys;
+    uint32_t* actors;
+    uint64_t* counters;
+    uint32_t* tomb_off;
+    uint64_t* tkeys;
+    uint32_t* tactors;
+    uint64_t* tcounters;
+};
+hipError_t launch_gen_delta(uint64_t seed, uint32_t n_docs, uint32_t R, uint32_t M, const OutView& D,
+                            const SrcOutView& S, hipStream_t stream);
 }  // namespace crdt
 
 using namespace crdt;
@@ -281,6 +296,23 @@ int crdt_gen_pair_async(crdt_ctx* ctx, uint64_t seed, uint32_t n_docs, const crd
     int rc = set_device(ctx);
     if (rc != CRDT_OK) return rc;
     return hip_err(launch_gen_pair(seed, n_docs, view(a), view(b), (hipStream_t)stream));
+}
+
+int crdt_gen_delta_async(crdt_ctx* ctx, uint64_t seed, uint32_t n_docs, uint32_t R, uint32_t n_srcs_per_doc,
+                         const crdt_awset_out* dst, const crdt_src_batch* srcs, void* stream) {
+    if (!ctx || !out_ptrs_ok(dst) || !src_ptrs_ok(srcs) || !srcs->tomb_off || R == 0 || R > CRDT_MAX_R ||
+        n_srcs_per_doc == 0)
+        return CRDT_E_INVALID;
+    if ((uint64_t)n_docs * n_srcs_per_doc * 8ull >= (1ull << 32) || (uint64_t)n_docs * 64ull >= (1ull << 32))
+        return CRDT_E_INVALID;
+    int rc = set_device(ctx);
+    if (rc != CRDT_OK) return rc;
+    auto w = [](const void* p) { return const_cast<void*>(p); };
+    SrcOutView S{(uint32_t*)w(srcs->doc_srcs), (uint32_t*)w(srcs->src_actor), (uint64_t*)w(srcs->vv),
+                 (uint32_t*)w(srcs->entry_off), (uint64_t*)w(srcs->keys), (uint32_t*)w(srcs->actors),
+                 (uint64_t*)w(srcs->counters), (uint32_t*)w(srcs->tomb_off), (uint64_t*)w(srcs->tkeys),
+                 (uint32_t*)w(srcs->tactors), (uint64_t*)w(srcs->tcounters)};
+    return hip_err(launch_gen_delta(seed, n_docs, R, n_srcs_per_doc, view(dst), S, (hipStream_t)stream));
 }
 
 /* ---------------- validation (host) ---------------- */

@@ -81,6 +81,131 @@ __global__ __launch_bounds__(WAVES * 64) void gen_pair_kernel(uint64_t seed, uin
     }
 }
 
+// ---------------------------------------------------------------------------
+// "delta" workload (BASELINE config 3): n_docs dst docs x 64 entries, R actors,
+// M ordered AWSetDelta sources per doc, each 8 entries + 2 tombstones.  Valid
+// random states with a controlled path mix (not simulated histories):
+//   H(d, tag, i) = splitmix64(seed ^ d << 20 ^ tag << 12 ^ i)
+//   universe u in [0, 256), key = d << 8 | u; a subset of size k is
+//   {u : (mul*u + add) & 255 < k}, mul odd, from one H draw
+//   dst: 64 keys, dot (H%R, 1 + (H>>8)%64), VV[r] = 64 + H%32
+//   1% of docs ("first contact"): dst VV[a*] = 0, no dst dot of actor a*,
+//   source 0 has actor a* -> full-merge path (awset-delta_test.go:53-56)
+//   source j: actor a_j = H%R, VV[r] = VV0[r] + 1 + H%16,
+//     8 entries: actor a_j (75%) or H%R; counter covered by VV0 (50%, pruned
+//     by MakeDeltaMergeData) or in (VV0, srcVV] (new)
+//     2 tombstones: actor a_j, counter srcVV[a_j] - H%8 (>= 1)
+// workloads.delta_docs restates these formulas on the host.
+__device__ __forceinline__ uint64_t Hx(uint64_t seed, uint64_t d, uint32_t tag, uint32_t i) {
+    return splitmix64(seed ^ (d << 20) ^ ((uint64_t)tag << 12) ^ (uint64_t)i);
+}
+
+struct SrcOutView {
+    uint32_t* doc_srcs;
+    uint32_t* src_actor;
+    uint64_t* vv;
+    uint32_t* entry_off;
+    uint64_t* keys;
+    uint32_t* actors;
+    uint64_t* counters;
+    uint32_t* tomb_off;
+    uint64_t* tkeys;
+    uint32_t* tactors;
+    uint64_t* tcounters;
+};
+
+// Writes the k-subset of the 256-key universe selected by draw h, sorted, at
+// base; f(u, slot) gives each selected key's fields.
+template <typename F>
+__device__ __forceinline__ void subset256(uint64_t h, uint32_t k, uint32_t lane, F f) {
+    const uint32_t mul = (uint32_t)(h & 0xFF) | 1u, add = (uint32_t)((h >> 8) & 0xFF);
+    uint32_t base = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const uint32_t u = q * 64 + lane;
+        const bool sel = ((mul * u + add) & 255u) < k;
+        const uint64_t m = ballot(sel);
+        if (sel) f(u, base + popc(m & low_mask(lane)));
+        base += popc(m);
+    }
+}
+
+template <int WAVES>
+__global__ __launch_bounds__(WAVES * 64) void gen_delta_kernel(uint64_t seed, uint32_t n_docs, uint32_t R, uint32_t M,
+                                                              OutView D, SrcOutView S) {
+    const uint32_t lane = threadIdx.x & 63;
+    for (uint32_t d0 = blockIdx.x * WAVES + (threadIdx.x >> 6); d0 < n_docs; d0 += gridDim.x * WAVES) {
+        const uint32_t d = uniform(d0);
+        const bool first = Hx(seed, d, 1, 0) % 100 == 0;
+        const uint32_t astar = (uint32_t)(Hx(seed, d, 1, 1) % R);
+        // dst VV0 (lane r)
+        uint64_t vv0 = 0;
+        if (lane < R) vv0 = (first && lane == astar) ? 0ull : 64 + Hx(seed, d, 3, lane) % 32;
+        subset256(Hx(seed, d, 0, 0), 64, lane, [&](uint32_t u, uint32_t slot) {
+            const uint64_t hu = Hx(seed, d, 2, u);
+            uint32_t a = (uint32_t)(hu % R);
+            if (first && a == astar) a = (a + 1) % R;
+            D.keys[(size_t)d * 64 + slot] = ((uint64_t)d << 8) | u;
+            D.actors[(size_t)d * 64 + slot] = a;
+            D.counters[(size_t)d * 64 + slot] = 1 + (hu >> 8) % 64;
+        });
+        if (lane < R) D.vv[(size_t)d * R + lane] = vv0;
+        if (lane == 0) {
+            D.offsets[d] = d * 64;
+            D.counts[d] = 64;
+            S.doc_srcs[d] = d * M;
+            if (d == n_docs - 1) {
+                D.offsets[n_docs] = n_docs * 64;
+                S.doc_srcs[n_docs] = n_docs * M;
+                S.entry_off[(size_t)n_docs * M] = n_docs * M * 8;
+                S.tomb_off[(size_t)n_docs * M] = n_docs * M * 2;
+            }
+        }
+        for (uint32_t j = 0; j < M; ++j) {
+            const uint32_t sidx = d * M + j;
+            const uint32_t aj = (first && j == 0) ? astar : (uint32_t)(Hx(seed, d, 4, j) % R);
+            uint64_t svv = 0;
+            if (lane < R) svv = vv0 + 1 + Hx(seed, d, 5, j * R + lane) % 16;
+            if (lane < R) S.vv[(size_t)sidx * R + lane] = svv;
+            const uint64_t svv_aj = __shfl(svv, (int)aj);
+            if (lane == 0) {
+                S.src_actor[sidx] = aj;
+                S.entry_off[sidx] = sidx * 8;
+                S.tomb_off[sidx] = sidx * 2;
+            }
+            subset256(Hx(seed, d, 6, j), 8, lane, [&](uint32_t u, uint32_t slot) {
+                const uint64_t he = Hx(seed, d, 7, j * 256 + u);
+                const uint32_t a = (he & 3) == 0 ? (uint32_t)((he >> 2) % R) : aj;
+                // VV0[a], srcVV[a] live in lane a: fetch through LDS-free shuffles
+                // is not possible inside a divergent lambda, so recompute them.
+                const uint64_t v0 = (first && a == astar) ? 0ull : 64 + Hx(seed, d, 3, a) % 32;
+                const uint64_t sv = v0 + 1 + Hx(seed, d, 5, j * R + a) % 16;
+                const uint64_t c = ((he >> 8) & 1) == 0 ? 1 + (he >> 16) % (v0 > 0 ? v0 : 1)
+                                                       : v0 + 1 + (he >> 16) % (sv - v0);
+                S.keys[(size_t)sidx * 8 + slot] = ((uint64_t)d << 8) | u;
+                S.actors[(size_t)sidx * 8 + slot] = a;
+                S.counters[(size_t)sidx * 8 + slot] = c;
+            });
+            subset256(Hx(seed, d, 8, j), 2, lane, [&](uint32_t u, uint32_t slot) {
+                const uint64_t ht = Hx(seed, d, 9, j * 256 + u);
+                const uint64_t back = ht % 8;
+                S.tkeys[(size_t)sidx * 2 + slot] = ((uint64_t)d << 8) | u;
+                S.tactors[(size_t)sidx * 2 + slot] = aj;
+                S.tcounters[(size_t)sidx * 2 + slot] = svv_aj > back ? svv_aj - back : 1;
+            });
+        }
+    }
+}
+
+hipError_t launch_gen_delta(uint64_t seed, uint32_t n_docs, uint32_t R, uint32_t M, const OutView& D,
+                            const SrcOutView& S, hipStream_t stream) {
+    if (n_docs == 0) return hipSuccess;
+    uint32_t grid = (n_docs + 3) / 4;
+    if (grid > (1u << 20)) grid = 1u << 20;
+    hipLaunchKernelGGL((gen_delta_kernel<4>), dim3(grid), dim3(256), 0, stream, seed, n_docs, R, M, D, S);
+    return hipGetLastError();
+}
+
 hipError_t launch_gen_pair(uint64_t seed, uint32_t n_docs, const OutView& A, const OutView& B, hipStream_t stream) {
     if (n_docs == 0) return hipSuccess;
     uint32_t grid = (n_docs + 3) / 4;

@@ -158,6 +158,12 @@ int crdt_causal_context_async(crdt_ctx* ctx, const uint64_t* vv, uint32_t n_docs
  * (formulas: go-crdt-playground_amd/csrc/gen.hip).  a/b need n_docs*64 slots. */
 int crdt_gen_pair_async(crdt_ctx* ctx, uint64_t seed, uint32_t n_docs, const crdt_awset_out* a,
                         const crdt_awset_out* b, void* stream);
+/* "delta" (BASELINE config 3): n_docs dst docs x 64 entries (64 slots each),
+ * R actors, n_srcs_per_doc ordered AWSetDelta sources per doc of 8 entries and
+ * 2 tombstones.  Writes through srcs' pointers (all must be allocated:
+ * n_docs*M sources, 8 and 2 slots each).  Formulas: csrc/gen.hip. */
+int crdt_gen_delta_async(crdt_ctx* ctx, uint64_t seed, uint32_t n_docs, uint32_t R, uint32_t n_srcs_per_doc,
+                         const crdt_awset_out* dst, const crdt_src_batch* srcs, void* stream);
 
 /* ---- host buffers, synchronous: copies in, runs, copies out ------------- */
 int crdt_awset_join_batch(crdt_ctx* ctx, const crdt_awset_batch* dst, const crdt_awset_batch* src,

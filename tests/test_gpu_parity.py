@@ -17,7 +17,7 @@ import pytest
 
 import crdtgpu
 from crdtgpu import CRDT_FOLD_AWSET, CRDT_FOLD_DELTA, workloads
-from crdtgpu.batch import OutBuffers
+from crdtgpu.batch import OutBuffers, SrcBuffers
 from helpers import GOLDEN, batch_of, out_doc, outs_equal, random_state, snap_entries, src_batch_of
 from oracle import oracle
 
@@ -54,6 +54,22 @@ def assert_same(got, want, n_docs, R):
         raise AssertionError("doc %s differs:\n gpu    %s\n oracle %s" % (
             bad, out_doc(got, bad, R) if bad >= 0 else got.offsets[:8],
             out_doc(want, bad, R) if bad >= 0 else want.offsets[:8]))
+
+
+def assert_same_all(got, want, n_docs, R):
+    """Vectorised bit-exact comparison of two outputs over every document."""
+    assert (np.asarray(got.offsets[: n_docs + 1]) == np.asarray(want.offsets[: n_docs + 1])).all(), "offsets"
+    assert (np.asarray(got.counts[:n_docs]) == np.asarray(want.counts[:n_docs])).all(), "counts"
+    assert (np.asarray(got.vv[: n_docs * R]) == np.asarray(want.vv[: n_docs * R])).all(), "vv"
+    cnt = np.asarray(want.counts[:n_docs]).astype(np.int64)
+    starts = np.asarray(want.offsets[:n_docs]).astype(np.int64)
+    idx = np.repeat(starts, cnt) + (np.arange(cnt.sum()) - np.repeat(np.cumsum(cnt) - cnt, cnt))
+    for f in ("keys", "actors", "counters"):
+        g, w = np.asarray(getattr(got, f))[idx], np.asarray(getattr(want, f))[idx]
+        if not (g == w).all():
+            bad = int(np.nonzero(g != w)[0][0])
+            doc = int(np.searchsorted(np.cumsum(cnt), bad, side="right"))
+            raise AssertionError("%s differ first at doc %d" % (f, doc))
 
 
 def join_case(rng, n_docs, R, size_fn, universe, max_c, actor_hi=None):
@@ -280,17 +296,15 @@ def test_config2_full_size(eng, torch):
     eng.join_async(a, b, oab)
     eng.join_async(b, a, oba)
     eng.sync()
-    # sample: exact vs the oracle on host-regenerated inputs
-    sample = sorted(set(random.Random(1).sample(range(n), 3000)) | {0, n - 1})
-    wa, wb = workloads.pair_docs(0x5EED, sample)
-    rc, want_ab = oracle.join(batch_of(2, wa), batch_of(2, wb))
-    assert rc == 0
-    rc, want_ba = oracle.join(batch_of(2, wb), batch_of(2, wa))
-    assert rc == 0
+    # every document exact vs the oracle run on the same (device-generated) inputs
+    ha, hb = host_out(A, torch).as_batch(), host_out(B, torch).as_batch()
     hab, hba = host_out(oab, torch), host_out(oba, torch)
-    for i, d in enumerate(sample):
-        assert out_doc(hab, d, 2) == out_doc(want_ab, i, 2), d
-        assert out_doc(hba, d, 2) == out_doc(want_ba, i, 2), d
+    rc, want_ab = oracle.join(ha, hb)
+    assert rc == 0
+    assert_same_all(hab, want_ab, n, 2)
+    rc, want_ba = oracle.join(hb, ha)
+    assert rc == 0
+    assert_same_all(hba, want_ba, n, 2)
     # all docs: slot bounds, element-set symmetry (A<-B and B<-A hold the same keys), VV = max
     offs = hab.offsets.astype(np.int64)
     assert (offs == np.arange(n + 1, dtype=np.int64) * 128).all()
@@ -319,3 +333,48 @@ def test_config2_full_size(eng, torch):
     assert (hxx.keys[idx2] == hab.keys[idx]).all()
     assert (hxx.actors[idx2] == hab.actors[idx]).all()
     assert (hxx.counters[idx2] == hab.counters[idx]).all()
+
+
+def host_src(S, torch):
+    torch.cuda.synchronize()
+    return S.numpy()
+
+
+def test_gen_delta_matches_host_restatement(eng, torch):
+    n, R, M = 3000, 16, 10
+    dev = torch.device("cuda:0")
+    D = OutBuffers(n, R, n * 64, device=dev)
+    S = SrcBuffers(R, n, n * M, n * M * 8, n * M * 2, device=dev)
+    eng.gen_delta_async(0x5EED, n, R, M, D, S)
+    eng.sync()
+    hd, hs = host_out(D, torch), host_src(S, torch)
+    docs = list(range(0, n, 29)) + [n - 1]
+    wd, ws = workloads.delta_docs(0x5EED, docs, R, M)
+    for i, d in enumerate(docs):
+        assert out_doc(hd, d, R) == wd[i]
+        for j, (a, vv, e, t) in enumerate(ws[i]):
+            k = d * M + j
+            assert int(hs.src_actor[k]) == a
+            assert hs.vv[k * R:(k + 1) * R].tolist() == vv
+            o, p = int(hs.entry_off[k]), int(hs.tomb_off[k])
+            assert list(zip(hs.keys[o:o + 8].tolist(), hs.actors[o:o + 8].tolist(), hs.counters[o:o + 8].tolist())) == e
+            assert list(zip(hs.tkeys[p:p + 2].tolist(), hs.tactors[p:p + 2].tolist(),
+                            hs.tcounters[p:p + 2].tolist())) == t
+
+
+def test_config3_full_size(eng, torch):
+    """1,048,576 docs x 64 entries, R=16, 10 ordered AWSetDelta sources each
+    (10,485,760 deltas): every document bit-exact vs the oracle on the same inputs."""
+    n, R, M = 1 << 20, 16, 10
+    dev = torch.device("cuda:0")
+    D = OutBuffers(n, R, n * 64, device=dev)
+    S = SrcBuffers(R, n, n * M, n * M * 8, n * M * 2, device=dev)
+    eng.gen_delta_async(0x5EED, n, R, M, D, S)
+    out = OutBuffers(n, R, n * 64 + n * M * 8, device=dev)
+    eng.reserve(n, out.slots)
+    eng.fold_async(CRDT_FOLD_DELTA, D.as_batch(), S, out)
+    eng.sync()
+    hd, hs = host_out(D, torch).as_batch(), host_src(S, torch)
+    rc, want = oracle.fold(CRDT_FOLD_DELTA, hd, hs)
+    assert rc == 0
+    assert_same_all(host_out(out, torch), want, n, R)

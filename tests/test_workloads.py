@@ -58,3 +58,21 @@ def test_byte_formulas():
     R = 16
     want = 20 * 64 + 8 * R + 4 + 10 * (20 * 10 + 8 * R + 12) + 20 * 100 + 8 * R + 4
     assert workloads.fold_bytes([64], [100], 80, 20, 10, R) == want
+
+
+def test_delta_workload_shape_and_mix():
+    dsts, srcs = workloads.delta_docs(0x5EED, list(range(300)), R=16, M=10)
+    covered = total = first = 0
+    for (ents, vv), chain in zip(dsts, srcs):
+        assert len(ents) == 64 and [k for k, _, _ in ents] == sorted(k for k, _, _ in ents)
+        assert all(a < 16 and c >= 1 for _, a, c in ents)
+        first += min(vv) == 0
+        assert len(chain) == 10
+        for actor, svv, e, t in chain:
+            assert len(e) == 8 and len(t) == 2 and actor < 16
+            assert [k for k, _, _ in e] == sorted(k for k, _, _ in e)
+            for _, a, c in e:
+                total += 1
+                covered += vv[a] >= c
+    assert 0.4 < covered / total < 0.6
+    assert 0 < first < 12
