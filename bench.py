@@ -1,17 +1,20 @@
 #!/usr/bin/env python3
-"""Benchmark: batched AWSet full-state join on MI355X (BASELINE config 2).
+"""Benchmark: batched AWSet / AWSetDelta merges on MI355X.
 
-Workload (per GPU, weak scaling): 1,048,576 independent documents x 2 replicas,
-64 entries per replica state, R = 2 (synthetic reachable states generated on
-the device: csrc/gen.hip).  One step = one pass of the hot path over the batch:
+Default workload = BASELINE config 2 (the metric's configuration), per GPU
+(weak scaling): 1,048,576 independent documents x 2 replicas, 64 entries per
+replica state, R = 2, synthetic reachable states generated on the device
+(csrc/gen.hip).  One step = one pass of the hot path over the batch:
   A <- B and B <- A for every document (2 merges per doc, crdt_awset_join_async),
   then the per-GPU causal-context summary (elementwise max of the output VVs),
   all-reduced (max, u64) across GPUs over RCCL when N > 1.
+--config 3: delta-state anti-entropy -- 10 ordered AWSetDelta sources folded
+  into each of 1,048,576 docs (R = 16): 10,485,760 merges per step.
 Inputs are resident in HBM before the timed region.  Metric: replica merges/s
-(whole job), with the join kernel's achieved algorithmic HBM bandwidth against
-the 8 TB/s roofline.
+(whole job), with the dominant kernel's achieved algorithmic HBM bandwidth
+against the 8 TB/s roofline and the C oracle timed on the host beside it.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2|3]
   torchrun --nproc-per-node N bench.py --gpus N ...   (one process per GPU)
 """
 
@@ -28,37 +31,191 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level table)
 
 
-def cpu_baseline(A, B, n_sample, budget_s):
-    """Time the C oracle (single thread, the 'port' baseline) on the first
-    n_sample docs of this rank's batch, both directions, repeated for ~budget_s."""
+def _np_copy(t, n, dt):
+    return t[:n].cpu().numpy().view(dt).copy()
+
+
+def _host_batch(o, n_sample, R):
+    """First n_sample docs of a device batch/output, as a host batch."""
     import numpy as np
 
     from crdtgpu.batch import AWSetBatch
-    from oracle import oracle
 
-    def host(o):
-        off = o.offsets[: n_sample + 1].cpu().numpy().view(np.uint32).copy()
-        cnt = o.counts[:n_sample].cpu().numpy().view(np.uint32).copy()
-        end = int(off[-1])
-        return AWSetBatch(2, off, o.keys[:end].cpu().numpy().view(np.uint64).copy(),
-                          o.actors[:end].cpu().numpy().view(np.uint32).copy(),
-                          o.counters[:end].cpu().numpy().view(np.uint64).copy(),
-                          o.vv[: 2 * n_sample].cpu().numpy().view(np.uint64).copy(), counts=cnt)
+    off = _np_copy(o.offsets, n_sample + 1, np.uint32)
+    end = int(off[-1])
+    return AWSetBatch(R, off, _np_copy(o.keys, end, np.uint64), _np_copy(o.actors, end, np.uint32),
+                      _np_copy(o.counters, end, np.uint64), _np_copy(o.vv, R * n_sample, np.uint64),
+                      counts=_np_copy(o.counts, n_sample, np.uint32))
 
-    ha, hb = host(A), host(B)
+
+def _time_cpu(fn, merges_per_call, budget_s):
     merges, t0 = 0, time.perf_counter()
     while True:
-        rc1, _ = oracle.join(ha, hb)
-        rc2, _ = oracle.join(hb, ha)
-        assert rc1 == 0 and rc2 == 0
-        merges += 2 * n_sample
+        fn()
+        merges += merges_per_call
         el = time.perf_counter() - t0
         if el >= budget_s:
-            break
-    return {"value": merges / el, "unit": "merges/s", "cores": 1, "kind": "port",
-            "sample": "first %d docs of the config-2 batch, both directions, C oracle (oracle/awset_oracle.c, "
-                      "sorted-array restatement of awset.go:107-161), 1 thread, %d merges in %.1f s "
-                      "(no Go toolchain on the box: the reference itself cannot run)" % (n_sample, merges, el)}
+            return merges, el
+
+
+class Config2:
+    """Full-state join, both directions (BASELINE configs[1])."""
+
+    R = 2
+    kernel = "join_wave_kernel"
+    metric = "replica-merges/sec (AWSet full-state join) + achieved HBM GB/s (% roofline)"
+
+    def __init__(self, eng, n, seed, dev, stream):
+        import torch
+
+        from crdtgpu.batch import OutBuffers
+
+        self.eng, self.n, self.stream = eng, n, stream
+        R = self.R
+        eng.reserve(n, 0)
+        eng.set_max_doc_entries(64)  # the pair workload holds exactly 64 entries per replica
+        self.A = OutBuffers(n, R, n * 64, device=dev)
+        self.B = OutBuffers(n, R, n * 64, device=dev)
+        eng.gen_pair_async(seed, n, self.A, self.B, stream=stream)
+        self.oab = OutBuffers(n, R, 2 * n * 64, device=dev)
+        self.oba = OutBuffers(n, R, 2 * n * 64, device=dev)
+        self.ctx_ab = torch.zeros(R, dtype=torch.int64, device=dev)
+        self.ctx_ba = torch.zeros(R, dtype=torch.int64, device=dev)
+        self.a, self.b = self.A.as_batch(), self.B.as_batch()
+        self.merges_per_step = 2 * n
+        self.n_events = 3
+
+    def step(self, ev=None):
+        """Both joins; returns the local causal-context summary tensor."""
+        s, eng, n, R = self.stream, self.eng, self.n, self.R
+        if ev is not None:
+            ev[0].record(s)
+        eng.join_async(self.a, self.b, self.oab, stream=s)
+        if ev is not None:
+            ev[1].record(s)
+        eng.join_async(self.b, self.a, self.oba, stream=s)
+        if ev is not None:
+            ev[2].record(s)
+        eng.causal_context_async(self.oab.vv, n, R, self.ctx_ab, stream=s)
+        eng.causal_context_async(self.oba.vv, n, R, self.ctx_ba, stream=s)
+        eng.vv_max_async(self.ctx_ab, self.ctx_ba, R, stream=s)
+        return self.ctx_ab
+
+    def launch_seconds(self, events, steps):
+        t_ab = sum(e[0].elapsed_time(e[1]) for e in events) / steps / 1e3
+        t_ba = sum(e[1].elapsed_time(e[2]) for e in events) / steps / 1e3
+        return (t_ab + t_ba) / 2
+
+    def bytes_per_launch(self):
+        from crdtgpu import workloads
+
+        cA, cB = self.A.counts.cpu().numpy(), self.B.counts.cpu().numpy()
+        b1 = workloads.join_bytes(cA, cB, self.oab.counts.cpu().numpy(), self.R)
+        b2 = workloads.join_bytes(cB, cA, self.oba.counts.cpu().numpy(), self.R)
+        return (b1 + b2) // 2
+
+    def describe(self, world):
+        return {"workload": "config2: %d docs/GPU x 2 replicas x 64 entries, R=2, full-state join both directions "
+                            "+ causal-context allreduce(max,u64)" % self.n,
+                "docs_per_gpu": self.n, "replicas": 2, "entries_per_replica": 64, "R": self.R,
+                "merges_per_step": self.merges_per_step * world, "parallelism": "doc-sharded x%d" % world}
+
+    def cpu_baseline(self, n_sample, budget_s):
+        from oracle import oracle
+
+        ha, hb = _host_batch(self.A, n_sample, self.R), _host_batch(self.B, n_sample, self.R)
+
+        def run():
+            rc1, _ = oracle.join(ha, hb)
+            rc2, _ = oracle.join(hb, ha)
+            assert rc1 == 0 and rc2 == 0
+
+        merges, el = _time_cpu(run, 2 * n_sample, budget_s)
+        return {"value": merges / el, "unit": "merges/s", "cores": 1, "kind": "port",
+                "sample": "first %d docs of the config-2 batch, both directions, C oracle (oracle/awset_oracle.c, "
+                          "sorted-array restatement of awset.go:107-161), 1 thread, %d merges in %.1f s "
+                          "(no Go toolchain on the box: the reference itself cannot run)" % (n_sample, merges, el)}
+
+
+class Config3:
+    """Delta-state anti-entropy: M ordered AWSetDelta sources folded per doc (BASELINE configs[2])."""
+
+    R = 16
+    M = 10
+    kernel = "fold_wave_kernel"
+    metric = "replica-merges/sec (AWSetDelta fold, config 3) + achieved HBM GB/s (% roofline)"
+
+    def __init__(self, eng, n, seed, dev, stream):
+        import torch
+
+        from crdtgpu.batch import OutBuffers, SrcBuffers
+
+        self.eng, self.n, self.stream = eng, n, stream
+        R, M = self.R, self.M
+        self.D = OutBuffers(n, R, n * 64, device=dev)
+        self.S = SrcBuffers(R, n, n * M, n * M * 8, n * M * 2, device=dev)
+        eng.gen_delta_async(seed, n, R, M, self.D, self.S, stream=stream)
+        self.out = OutBuffers(n, R, n * 64 + n * M * 8, device=dev)
+        eng.reserve(n, self.out.slots)
+        self.ctx = torch.zeros(R, dtype=torch.int64, device=dev)
+        self.d = self.D.as_batch()
+        self.merges_per_step = n * M
+        self.n_events = 2
+
+    def step(self, ev=None):
+        import crdtgpu
+
+        s = self.stream
+        if ev is not None:
+            ev[0].record(s)
+        self.eng.fold_async(crdtgpu.CRDT_FOLD_DELTA, self.d, self.S, self.out, stream=s)
+        if ev is not None:
+            ev[1].record(s)
+        self.eng.causal_context_async(self.out.vv, self.n, self.R, self.ctx, stream=s)
+        return self.ctx
+
+    def launch_seconds(self, events, steps):
+        return sum(e[0].elapsed_time(e[1]) for e in events) / steps / 1e3
+
+    def bytes_per_launch(self):
+        from crdtgpu import workloads
+
+        n, M = self.n, self.M
+        return workloads.fold_bytes(self.D.counts.cpu().numpy(), self.out.counts.cpu().numpy(), n * M * 8,
+                                    n * M * 2, n * M, self.R)
+
+    def describe(self, world):
+        return {"workload": "config3: %d dst docs/GPU x 64 entries, R=16, %d ordered AWSetDelta sources per doc "
+                            "(8 entries + 2 tombstones each), delta fold" % (self.n, self.M),
+                "docs_per_gpu": self.n, "deltas_per_doc": self.M, "R": self.R,
+                "merges_per_step": self.merges_per_step * world, "parallelism": "doc-sharded x%d" % world}
+
+    def cpu_baseline(self, n_sample, budget_s):
+        import numpy as np
+
+        import crdtgpu
+        from crdtgpu.batch import SrcBatch
+        from oracle import oracle
+
+        M, R, S = self.M, self.R, self.S
+        hd = _host_batch(self.D, n_sample, R)
+        k = n_sample * M
+        u32, u64 = np.uint32, np.uint64
+        hs = SrcBatch(R, _np_copy(S.doc_srcs, n_sample + 1, u32), _np_copy(S.src_actor, k, u32),
+                      _np_copy(S.vv, k * R, u64), _np_copy(S.entry_off, k + 1, u32), _np_copy(S.keys, k * 8, u64),
+                      _np_copy(S.actors, k * 8, u32), _np_copy(S.counters, k * 8, u64),
+                      _np_copy(S.tomb_off, k + 1, u32), _np_copy(S.tkeys, k * 2, u64),
+                      _np_copy(S.tactors, k * 2, u32), _np_copy(S.tcounters, k * 2, u64))
+
+        def run():
+            rc, _ = oracle.fold(crdtgpu.CRDT_FOLD_DELTA, hd, hs)
+            assert rc == 0
+
+        merges, el = _time_cpu(run, k, budget_s)
+        return {"value": merges / el, "unit": "merges/s", "cores": 1, "kind": "port",
+                "sample": "first %d docs of the config-3 batch (%d deltas), C oracle (oracle/awset_oracle.c, "
+                          "restatement of awset-delta_test.go:51-166), 1 thread, %d merges in %.1f s" % (
+                              n_sample, k, merges, el)}
 
 
 def main():
@@ -66,6 +223,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", type=int, default=2, choices=[2, 3])
     ap.add_argument("--docs", type=int, default=1 << 20, help="documents per GPU")
     ap.add_argument("--seed", type=int, default=0x5EED)
     ap.add_argument("--cpu-sample", type=int, default=65536)
@@ -78,8 +236,6 @@ def main():
     import torch
 
     import crdtgpu
-    from crdtgpu.batch import OutBuffers
-    from crdtgpu import workloads
     from crdtgpu.dist import u64_max_allreduce
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -96,56 +252,29 @@ def main():
     stream = torch.cuda.current_stream()
 
     n = args.docs
-    R = 2
     eng = crdtgpu.Engine(local)
-    eng.reserve(n, 0)
-    eng.set_max_doc_entries(64)  # the pair workload holds exactly 64 entries per replica
     # each rank owns its own documents (weak scaling; no data-path exchange)
     seed = args.seed + (rank << 40)
-    A = OutBuffers(n, R, n * 64, device=dev)
-    B = OutBuffers(n, R, n * 64, device=dev)
-    eng.gen_pair_async(seed, n, A, B, stream=stream)
-    oab = OutBuffers(n, R, 2 * n * 64, device=dev)
-    oba = OutBuffers(n, R, 2 * n * 64, device=dev)
-    ctx_ab = torch.zeros(R, dtype=torch.int64, device=dev)
-    ctx_ba = torch.zeros(R, dtype=torch.int64, device=dev)
-    a, b = A.as_batch(), B.as_batch()
+    W = {2: Config2, 3: Config3}[args.config](eng, n, seed, dev, stream)
     eng.sync(stream)
 
     def step(ev=None):
-        if ev is not None:
-            ev[0].record(stream)
-        eng.join_async(a, b, oab, stream=stream)
-        if ev is not None:
-            ev[1].record(stream)
-        eng.join_async(b, a, oba, stream=stream)
-        if ev is not None:
-            ev[2].record(stream)
-        eng.causal_context_async(oab.vv, n, R, ctx_ab, stream=stream)
-        eng.causal_context_async(oba.vv, n, R, ctx_ba, stream=stream)
-        eng.vv_max_async(ctx_ab, ctx_ba, R, stream=stream)
+        local_ctx = W.step(ev)
         if dist is not None:
-            return u64_max_allreduce(dist, ctx_ab)
-        return ctx_ab
+            return u64_max_allreduce(dist, local_ctx)
+        return local_ctx
 
     for _ in range(args.warmup):
         step()
     eng.sync(stream)
+    bytes_launch = W.bytes_per_launch()  # algorithmic bytes from the actual output sizes
 
-    # algorithmic bytes per join launch, from the actual output sizes
-    n_out_ab = int(oab.counts.to(torch.int64).sum().item())
-    n_out_ba = int(oba.counts.to(torch.int64).sum().item())
-    n_in = int(A.counts.to(torch.int64).sum().item()), int(B.counts.to(torch.int64).sum().item())
-    bytes_ab = 20 * (n_in[0] + n_in[1] + n_out_ab) + (24 * R + 12) * n
-    bytes_ba = 20 * (n_in[0] + n_in[1] + n_out_ba) + (24 * R + 12) * n
-    assert bytes_ab == workloads.join_bytes(A.counts.cpu().numpy(), B.counts.cpu().numpy(),
-                                            oab.counts.cpu().numpy(), R)
-
-    events = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+    events = [[torch.cuda.Event(enable_timing=True) for _ in range(W.n_events)] for _ in range(args.steps)]
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    g = None
     for k in range(args.steps):
         g = step(events[k])
     torch.cuda.synchronize()
@@ -158,24 +287,22 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    t_ab = sum(e[0].elapsed_time(e[1]) for e in events) / args.steps / 1e3  # s per launch
-    t_ba = sum(e[1].elapsed_time(e[2]) for e in events) / args.steps / 1e3
-    t_launch = (t_ab + t_ba) / 2
-    achieved = (bytes_ab + bytes_ba) / 2 / t_launch / 1e9
-    global_ctx = g.cpu().numpy().view(np.uint64).tolist()
+    t_launch = W.launch_seconds(events, args.steps)
+    achieved = bytes_launch / t_launch / 1e9
+    global_ctx = g.cpu().numpy().view(np.uint64).tolist() if g is not None else []
 
-    merges = 2 * n * world * args.steps
     traffic = None
     if os.path.exists(args.traffic_json):
         try:
             tj = json.load(open(args.traffic_json))
-            if tj.get("docs") == n and tj.get("kernel", "").startswith("join_wave_kernel"):
+            if tj.get("docs") == n and tj.get("kernel", "").startswith(W.kernel):
                 traffic = tj.get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
 
+    merges = W.merges_per_step * world * args.steps
     result = {
-        "metric": "replica-merges/sec (AWSet full-state join) + achieved HBM GB/s (% roofline)",
+        "metric": W.metric,
         "value": merges / elapsed,
         "unit": "merges/s",
         "n_gpus": world,
@@ -186,24 +313,17 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "u64",
-        "data": "synthetic (reachable AWSet states generated on device, csrc/gen.hip)",
-        "config": {
-            "workload": "config2: %d docs/GPU x 2 replicas x 64 entries, R=2, full-state join both directions "
-                        "+ causal-context allreduce(max,u64)" % n,
-            "docs_per_gpu": n, "replicas": 2, "entries_per_replica": 64, "R": R,
-            "merges_per_step": 2 * n * world, "parallelism": "doc-sharded x%d" % world,
-        },
+        "data": "synthetic (AWSet states generated on device, csrc/gen.hip)",
+        "config": W.describe(world),
         "roofline": {
             "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-            "kernel": "join_wave_kernel<4>",
-            "algorithmic_bytes_per_launch": (bytes_ab + bytes_ba) // 2,
-            "launch_ms": t_launch * 1e3,
+            "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": W.kernel,
+            "algorithmic_bytes_per_launch": bytes_launch, "launch_ms": t_launch * 1e3,
         },
         "global_causal_context": global_ctx,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        result["cpu_baseline"] = cpu_baseline(A, B, min(args.cpu_sample, n), args.cpu_budget)
+        result["cpu_baseline"] = W.cpu_baseline(min(args.cpu_sample, n), args.cpu_budget)
     if rank == 0:
         print(json.dumps(result), flush=True)
     eng.close()
