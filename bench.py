@@ -10,11 +10,13 @@ replica state, R = 2, synthetic reachable states generated on the device
   all-reduced (max, u64) across GPUs over RCCL when N > 1.
 --config 3: delta-state anti-entropy -- 10 ordered AWSetDelta sources folded
   into each of 1,048,576 docs (R = 16): 10,485,760 merges per step.
+--config 5: 12.5M docs per GPU (100M over 8 GPUs) x 8 replicas of 16 entries
+  (R = 8) folded r0 <- r1 <- ... <- r7, plus the global causal context.
 Inputs are resident in HBM before the timed region.  Metric: replica merges/s
 (whole job), with the dominant kernel's achieved algorithmic HBM bandwidth
 against the 8 TB/s roofline and the C oracle timed on the host beside it.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2|3]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2|3|5]
   torchrun --nproc-per-node N bench.py --gpus N ...   (one process per GPU)
 """
 
@@ -218,13 +220,95 @@ class Config3:
                               n_sample, k, merges, el)}
 
 
+class Config5:
+    """100M docs x 8 replicas over 8 GPUs (BASELINE configs[4]): per GPU 12.5M docs,
+    8 AWSet states of 16 entries (R = 8) folded r0 <- r1 <- ... <- r7 (7 merges
+    per doc), then the global causal context: per-GPU VV max + RCCL all-reduce."""
+
+    R = P = 8
+    E = 16
+    kernel = "fold_wave_kernel"
+    metric = "replica-merges/sec (AWSet fold r0<-..<-r7, config 5) + achieved HBM GB/s (% roofline)"
+
+    def __init__(self, eng, n, seed, dev, stream):
+        import torch
+
+        from crdtgpu.batch import OutBuffers, SrcBuffers
+
+        self.eng, self.n, self.stream = eng, n, stream
+        P, E, R = self.P, self.E, self.R
+        self.D = OutBuffers(n, R, n * E, device=dev)
+        self.S = SrcBuffers(R, n, n * (P - 1), n * (P - 1) * E, 0, device=dev)
+        eng.gen_replicas_async(seed, n, P, E, self.D, self.S, stream=stream)
+        self.out = OutBuffers(n, R, n * E * P, device=dev)
+        # a doc never exceeds 16 + 7*16 = 128 slots: it stays on the LDS wave path
+        eng.reserve(n, 0)
+        self.ctx = torch.zeros(R, dtype=torch.int64, device=dev)
+        self.d = self.D.as_batch()
+        self.merges_per_step = n * (P - 1)
+        self.n_events = 2
+
+    def step(self, ev=None):
+        import crdtgpu
+
+        s = self.stream
+        if ev is not None:
+            ev[0].record(s)
+        self.eng.fold_async(crdtgpu.CRDT_FOLD_AWSET, self.d, self.S, self.out, stream=s)
+        if ev is not None:
+            ev[1].record(s)
+        self.eng.causal_context_async(self.out.vv, self.n, self.R, self.ctx, stream=s)
+        return self.ctx
+
+    def launch_seconds(self, events, steps):
+        return sum(e[0].elapsed_time(e[1]) for e in events) / steps / 1e3
+
+    def bytes_per_launch(self):
+        from crdtgpu import workloads
+
+        n, P, E = self.n, self.P, self.E
+        return workloads.fold_bytes(self.D.counts.cpu().numpy(), self.out.counts.cpu().numpy(), n * (P - 1) * E, 0,
+                                    n * (P - 1), self.R)
+
+    def describe(self, world):
+        return {"workload": "config5: %d docs/GPU x 8 replicas x 16 entries, R=8, fold r0<-r1<-..<-r7 + global "
+                            "causal-context allreduce(max,u64) over RCCL" % self.n,
+                "docs_per_gpu": self.n, "replicas": self.P, "entries_per_replica": self.E, "R": self.R,
+                "merges_per_step": self.merges_per_step * world, "parallelism": "doc-sharded x%d" % world}
+
+    def cpu_baseline(self, n_sample, budget_s):
+        import numpy as np
+
+        import crdtgpu
+        from crdtgpu.batch import SrcBatch
+        from oracle import oracle
+
+        P, E, R, S = self.P, self.E, self.R, self.S
+        hd = _host_batch(self.D, n_sample, R)
+        k = n_sample * (P - 1)
+        u32, u64 = np.uint32, np.uint64
+        hs = SrcBatch(R, _np_copy(S.doc_srcs, n_sample + 1, u32), _np_copy(S.src_actor, k, u32),
+                      _np_copy(S.vv, k * R, u64), _np_copy(S.entry_off, k + 1, u32), _np_copy(S.keys, k * E, u64),
+                      _np_copy(S.actors, k * E, u32), _np_copy(S.counters, k * E, u64))
+
+        def run():
+            rc, _ = oracle.fold(crdtgpu.CRDT_FOLD_AWSET, hd, hs)
+            assert rc == 0
+
+        merges, el = _time_cpu(run, k, budget_s)
+        return {"value": merges / el, "unit": "merges/s", "cores": 1, "kind": "port",
+                "sample": "first %d docs of the config-5 batch (%d merges per pass), C oracle (oracle/awset_oracle.c, "
+                          "restatement of awset.go:107-161), 1 thread, %d merges in %.1f s" % (n_sample, k, merges, el)}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--config", type=int, default=2, choices=[2, 3])
-    ap.add_argument("--docs", type=int, default=1 << 20, help="documents per GPU")
+    ap.add_argument("--config", type=int, default=2, choices=[2, 3, 5])
+    ap.add_argument("--docs", type=int, default=None,
+                    help="documents per GPU (default 1,048,576; config 5: 12,500,000 = 100M / 8)")
     ap.add_argument("--seed", type=int, default=0x5EED)
     ap.add_argument("--cpu-sample", type=int, default=65536)
     ap.add_argument("--cpu-budget", type=float, default=12.0)
@@ -251,11 +335,11 @@ def main():
     torch.cuda.set_device(dev)
     stream = torch.cuda.current_stream()
 
-    n = args.docs
+    n = args.docs or (12_500_000 if args.config == 5 else 1 << 20)
     eng = crdtgpu.Engine(local)
     # each rank owns its own documents (weak scaling; no data-path exchange)
     seed = args.seed + (rank << 40)
-    W = {2: Config2, 3: Config3}[args.config](eng, n, seed, dev, stream)
+    W = {2: Config2, 3: Config3, 5: Config5}[args.config](eng, n, seed, dev, stream)
     eng.sync(stream)
 
     def step(ev=None):

@@ -84,6 +84,12 @@ class Engine:
         check(self._lib.crdt_gen_delta_async(self._ctx, int(seed), int(n_docs), int(R), int(M), ctypes.byref(cd),
                                              ctypes.byref(cs), _stream(stream)), "crdt_gen_delta_async")
 
+    def gen_replicas_async(self, seed: int, n_docs: int, P: int, E: int, dst: OutBuffers, srcs: SrcBatch,
+                           stream=None):
+        cd, cs = dst.c(), srcs.c()
+        check(self._lib.crdt_gen_replicas_async(self._ctx, int(seed), int(n_docs), int(P), int(E), ctypes.byref(cd),
+                                                ctypes.byref(cs), _stream(stream)), "crdt_gen_replicas_async")
+
     # -- host buffers, synchronous ----------------------------------------
     def join(self, dst: AWSetBatch, src: AWSetBatch) -> OutBuffers:
         dst, src = dst.numpy(), src.numpy()

@@ -109,6 +109,35 @@ def delta_docs(seed: int, docs, R: int = 16, M: int = 10):
     return dsts, srcs
 
 
+def replica_docs(seed: int, docs, P: int = 8, E: int = 16):
+    """Host copy of the "replicas" workload (csrc/gen.hip): (dst docs = replica 0,
+    per-doc sources = replicas 1..P-1 as (actor, vv, entries, []))."""
+    U, R = 2 * E, P
+    dsts, srcs = [], []
+    for d in docs:
+        chain = []
+        for r in range(P):
+            vv = [E + _H(seed, d, 20, r * 64 + a) % E if a == r else _H(seed, d, 20, r * 64 + a) % (E + E // 2)
+                  for a in range(R)]
+            h = _H(seed, d, 21, r)
+            mul, add = (h & 0xFF) | 1, (h >> 8) & 0xFF
+            ents = []
+            for u in range(U):
+                if ((mul * u + add) & (U - 1)) >= E:
+                    continue
+                he = _H(seed, d, 22, r * 64 + u)
+                a = (he >> 2) % R if (he & 3) == 0 else r
+                if vv[a] == 0:
+                    a = r
+                ents.append(((d << 8) | u, a, 1 + (he >> 16) % vv[a]))
+            if r == 0:
+                dsts.append((ents, vv))
+            else:
+                chain.append((r, vv, ents, []))
+        srcs.append(chain)
+    return dsts, srcs
+
+
 def join_bytes(n_dst, n_src, n_out, R) -> int:
     """Σ over docs of 20(n_dst + n_src + n_out) + 24R + 12."""
     n_dst, n_src, n_out = (np.asarray(x, dtype=np.int64) for x in (n_dst, n_src, n_out))

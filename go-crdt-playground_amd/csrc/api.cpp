@@ -35,6 +35,8 @@ struct SrcOutView {
 };
 hipError_t launch_gen_delta(uint64_t seed, uint32_t n_docs, uint32_t R, uint32_t M, const OutView& D,
                             const SrcOutView& S, hipStream_t stream);
+hipError_t launch_gen_replicas(uint64_t seed, uint32_t n_docs, uint32_t P, uint32_t E, const OutView& D,
+                               const SrcOutView& S, hipStream_t stream);
 }  // namespace crdt
 
 using namespace crdt;
@@ -313,6 +315,22 @@ int crdt_gen_delta_async(crdt_ctx* ctx, uint64_t seed, uint32_t n_docs, uint32_t
                  (uint64_t*)w(srcs->counters), (uint32_t*)w(srcs->tomb_off), (uint64_t*)w(srcs->tkeys),
                  (uint32_t*)w(srcs->tactors), (uint64_t*)w(srcs->tcounters)};
     return hip_err(launch_gen_delta(seed, n_docs, R, n_srcs_per_doc, view(dst), S, (hipStream_t)stream));
+}
+
+int crdt_gen_replicas_async(crdt_ctx* ctx, uint64_t seed, uint32_t n_docs, uint32_t replicas, uint32_t entries,
+                            const crdt_awset_out* dst, const crdt_src_batch* srcs, void* stream) {
+    if (!ctx || !out_ptrs_ok(dst) || !src_ptrs_ok(srcs) || !srcs->tomb_off) return CRDT_E_INVALID;
+    if (replicas < 2 || replicas > CRDT_MAX_R || entries < 1 || entries > 32 || (entries & (entries - 1)))
+        return CRDT_E_INVALID;
+    if ((uint64_t)n_docs * replicas * entries >= (1ull << 32)) return CRDT_E_INVALID;
+    int rc = set_device(ctx);
+    if (rc != CRDT_OK) return rc;
+    auto w = [](const void* p) { return const_cast<void*>(p); };
+    SrcOutView S{(uint32_t*)w(srcs->doc_srcs), (uint32_t*)w(srcs->src_actor), (uint64_t*)w(srcs->vv),
+                 (uint32_t*)w(srcs->entry_off), (uint64_t*)w(srcs->keys), (uint32_t*)w(srcs->actors),
+                 (uint64_t*)w(srcs->counters), (uint32_t*)w(srcs->tomb_off), (uint64_t*)w(srcs->tkeys),
+                 (uint32_t*)w(srcs->tactors), (uint64_t*)w(srcs->tcounters)};
+    return hip_err(launch_gen_replicas(seed, n_docs, replicas, entries, view(dst), S, (hipStream_t)stream));
 }
 
 /* ---------------- validation (host) ---------------- */

@@ -206,6 +206,88 @@ hipError_t launch_gen_delta(uint64_t seed, uint32_t n_docs, uint32_t R, uint32_t
     return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------
+// "replicas" workload (BASELINE config 5): per document, P replica states of E
+// entries each over R = P actors, to be folded r0 <- r1 <- ... <- r(P-1).
+//   universe u in [0, 2E), key = d << 8 | u; replica r holds the E keys
+//   {u : (mul*u + add) mod 2E < E} (mul odd, one H draw; 2E a power of two)
+//   replica r's VV: own VV[r] = E + H%E, others VV[a] = H % (E + E/2)
+//   each entry's dot: actor r (75%) or H%R when that actor's VV > 0, counter
+//   1 + H % VV[actor] (covered by the replica's own clock)
+// dst = replica 0 (batch D), sources = replicas 1..P-1 (batch S, no tombstones).
+// workloads.replica_docs restates these formulas on the host.
+template <int WAVES>
+__global__ __launch_bounds__(WAVES * 64) void gen_replicas_kernel(uint64_t seed, uint32_t n_docs, uint32_t P,
+                                                                 uint32_t E, OutView D, SrcOutView S) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t U = 2 * E;  // universe, power of two, <= 64
+    const uint32_t R = P;
+    for (uint32_t d0 = blockIdx.x * WAVES + (threadIdx.x >> 6); d0 < n_docs; d0 += gridDim.x * WAVES) {
+        const uint32_t d = uniform(d0);
+        if (lane == 0) {
+            D.offsets[d] = d * E;
+            D.counts[d] = E;
+            S.doc_srcs[d] = d * (P - 1);
+            if (d == n_docs - 1) {
+                D.offsets[n_docs] = n_docs * E;
+                S.doc_srcs[n_docs] = n_docs * (P - 1);
+                S.entry_off[(size_t)n_docs * (P - 1)] = n_docs * (P - 1) * E;
+                S.tomb_off[(size_t)n_docs * (P - 1)] = 0;
+            }
+        }
+        for (uint32_t r = 0; r < P; ++r) {
+            // VV of replica r: lane a holds VV[a]
+            uint64_t vv = 0;
+            if (lane < R) vv = lane == r ? E + Hx(seed, d, 20, r * 64 + lane) % E : Hx(seed, d, 20, r * 64 + lane) % (E + E / 2);
+            const uint64_t h = Hx(seed, d, 21, r);
+            const uint32_t mul = (uint32_t)(h & 0xFF) | 1u, add = (uint32_t)((h >> 8) & 0xFF);
+            const uint32_t u = lane;
+            const bool sel = u < U && ((mul * u + add) & (U - 1)) < E;
+            const uint64_t m = ballot(sel);
+            const uint32_t slot = popc(m & low_mask(lane));
+            const uint64_t he = Hx(seed, d, 22, r * 64 + u);
+            uint32_t a = (he & 3) == 0 ? (uint32_t)((he >> 2) % R) : r;
+            uint64_t va = __shfl(vv, (int)a);
+            if (va == 0) {  // never seen that actor: fall back to own dot
+                a = r;
+                va = __shfl(vv, (int)r);
+            }
+            const uint64_t c = 1 + (he >> 16) % va;
+            const uint64_t key = ((uint64_t)d << 8) | u;
+            if (r == 0) {
+                if (sel) {
+                    D.keys[(size_t)d * E + slot] = key;
+                    D.actors[(size_t)d * E + slot] = a;
+                    D.counters[(size_t)d * E + slot] = c;
+                }
+                if (lane < R) D.vv[(size_t)d * R + lane] = vv;
+            } else {
+                const size_t sidx = (size_t)d * (P - 1) + (r - 1);
+                if (sel) {
+                    S.keys[sidx * E + slot] = key;
+                    S.actors[sidx * E + slot] = a;
+                    S.counters[sidx * E + slot] = c;
+                }
+                if (lane < R) S.vv[sidx * R + lane] = vv;
+                if (lane == 0) {
+                    S.src_actor[sidx] = r;
+                    S.entry_off[sidx] = (uint32_t)(sidx * E);
+                    S.tomb_off[sidx] = 0;
+                }
+            }
+        }
+    }
+}
+
+hipError_t launch_gen_replicas(uint64_t seed, uint32_t n_docs, uint32_t P, uint32_t E, const OutView& D,
+                               const SrcOutView& S, hipStream_t stream) {
+    if (n_docs == 0) return hipSuccess;
+    uint32_t grid = (n_docs + 3) / 4;
+    if (grid > (1u << 20)) grid = 1u << 20;
+    hipLaunchKernelGGL((gen_replicas_kernel<4>), dim3(grid), dim3(256), 0, stream, seed, n_docs, P, E, D, S);
+    return hipGetLastError();
+}
+
 hipError_t launch_gen_pair(uint64_t seed, uint32_t n_docs, const OutView& A, const OutView& B, hipStream_t stream) {
     if (n_docs == 0) return hipSuccess;
     uint32_t grid = (n_docs + 3) / 4;

@@ -164,6 +164,12 @@ int crdt_gen_pair_async(crdt_ctx* ctx, uint64_t seed, uint32_t n_docs, const crd
  * n_docs*M sources, 8 and 2 slots each).  Formulas: csrc/gen.hip. */
 int crdt_gen_delta_async(crdt_ctx* ctx, uint64_t seed, uint32_t n_docs, uint32_t R, uint32_t n_srcs_per_doc,
                          const crdt_awset_out* dst, const crdt_src_batch* srcs, void* stream);
+/* "replicas" (BASELINE config 5): per doc `replicas` AWSet states of `entries`
+ * entries (a power of two <= 32), R = replicas; dst = replica 0 (entries slots
+ * per doc), srcs = replicas 1.. in order (entries slots each, 0 tombstones;
+ * tomb_off must be allocated).  Fold with CRDT_FOLD_AWSET. */
+int crdt_gen_replicas_async(crdt_ctx* ctx, uint64_t seed, uint32_t n_docs, uint32_t replicas, uint32_t entries,
+                            const crdt_awset_out* dst, const crdt_src_batch* srcs, void* stream);
 
 /* ---- host buffers, synchronous: copies in, runs, copies out ------------- */
 int crdt_awset_join_batch(crdt_ctx* ctx, const crdt_awset_batch* dst, const crdt_awset_batch* src,

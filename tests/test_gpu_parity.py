@@ -378,3 +378,35 @@ def test_config3_full_size(eng, torch):
     rc, want = oracle.fold(CRDT_FOLD_DELTA, hd, hs)
     assert rc == 0
     assert_same_all(host_out(out, torch), want, n, R)
+
+
+def test_gen_replicas_and_config5_fold(eng, torch):
+    """Config 5 shape (8 replicas x 16 entries, R=8, fold r0<-..<-r7) on 1,048,576
+    docs: generator vs host restatement on a sample; every doc's fold exact vs
+    the oracle; the causal-context summary vs the oracle."""
+    n, P, E, R = 1 << 20, 8, 16, 8
+    dev = torch.device("cuda:0")
+    D = OutBuffers(n, R, n * E, device=dev)
+    S = SrcBuffers(R, n, n * (P - 1), n * (P - 1) * E, 0, device=dev)
+    eng.gen_replicas_async(0x5EED, n, P, E, D, S)
+    out = OutBuffers(n, R, n * E * P, device=dev)
+    eng.fold_async(CRDT_FOLD_AWSET, D.as_batch(), S, out)
+    ctx = torch.zeros(R, dtype=torch.int64, device=dev)
+    eng.causal_context_async(out.vv, n, R, ctx)
+    eng.sync()
+    hd, hs = host_out(D, torch), host_src(S, torch)
+    docs = list(range(0, n, 104729)) + [n - 1]
+    wd, ws = workloads.replica_docs(0x5EED, docs, P, E)
+    for i, d in enumerate(docs):
+        assert out_doc(hd, d, R) == wd[i]
+        for j, (a, vv, e, _) in enumerate(ws[i]):
+            k = d * (P - 1) + j
+            assert int(hs.src_actor[k]) == a and hs.vv[k * R:(k + 1) * R].tolist() == vv
+            o = int(hs.entry_off[k])
+            assert list(zip(hs.keys[o:o + E].tolist(), hs.actors[o:o + E].tolist(),
+                            hs.counters[o:o + E].tolist())) == e
+    rc, want = oracle.fold(CRDT_FOLD_AWSET, hd.as_batch(), hs)
+    assert rc == 0
+    ho = host_out(out, torch)
+    assert_same_all(ho, want, n, R)
+    assert ctx.cpu().numpy().view(np.uint64).tolist() == oracle.causal_context(want.vv, n, R).tolist()

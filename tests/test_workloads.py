@@ -76,3 +76,14 @@ def test_delta_workload_shape_and_mix():
                 covered += vv[a] >= c
     assert 0.4 < covered / total < 0.6
     assert 0 < first < 12
+
+
+def test_replica_workload_is_consistent():
+    """Config 5 states: every dot is covered by its own replica's clock, E keys each."""
+    dsts, srcs = workloads.replica_docs(0x5EED, list(range(200)), P=8, E=16)
+    for (ents, vv), chain in zip(dsts, srcs):
+        states = [(0, vv, ents, [])] + chain
+        assert [c[0] for c in states] == list(range(8))
+        for r, v, e, t in states:
+            assert len(e) == 16 and not t and v[r] >= 16
+            assert all(v[a] >= c >= 1 for _, a, c in e)
