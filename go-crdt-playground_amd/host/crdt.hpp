@@ -1,0 +1,355 @@
+// crdt.hpp -- C++ host mirror of the reference's Go API, merging on the GPU.
+//
+// Same types and method names as package crdt (rsms/go-crdt-playground):
+//   Actor, Dot                        crdt-misc.go:8-19
+//   VersionVector                     crdt-misc.go:21-74
+//   AWSet                             awset.go:55-171
+//   AWSetDelta                        awset-delta_test.go:9-77
+// Merge() and the batch entry points (MergeBatch, FoldBatch, DeltaMergeBatch)
+// intern the string keys of the batch into order-preserving u64 ids, pack the
+// structure-of-arrays buffers of include/crdtgpu.h, run the HIP kernels through
+// crdt_awset_join_batch / crdt_awset_fold_batch and unpack the result.  Local
+// ops (Add, Del, Clone, ...) are per-replica host state, as in the reference.
+//
+// Where the Go code panics (HasDot/Counter at actor == len(vv), Add with the
+// actor outside the vector), this API throws crdt::Error carrying the C ABI
+// code (CRDT_E_ACTOR_RANGE); a failed merge leaves its destinations untouched.
+// Version vectors of one batch are zero-padded to the longest (<= 64).
+#pragma once
+
+#include <algorithm>
+#include <cstdint>
+#include <map>
+#include <stdexcept>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/crdtgpu.h"
+
+namespace crdt {
+
+using Actor = uint32_t;  // crdt-misc.go:9 (uint; the engine stores u32 actors)
+
+struct Error : std::runtime_error {
+    int code;
+    Error(int c, const std::string& what) : std::runtime_error(what + ": " + crdt_strerror(c)), code(c) {}
+};
+
+inline void check(int rc, const char* what) {
+    if (rc != CRDT_OK) throw Error(rc, what);
+}
+
+// crdt-misc.go:12-19
+struct Dot {
+    Actor actor = 0;
+    uint64_t counter = 0;
+    bool operator==(const Dot& o) const { return actor == o.actor && counter == o.counter; }
+    bool operator!=(const Dot& o) const { return !(*this == o); }
+    std::string String() const { return "(" + std::string(1, char('A' + actor)) + " " + std::to_string(counter) + ")"; }
+};
+
+// crdt-misc.go:23-74
+struct VersionVector : std::vector<uint64_t> {
+    using std::vector<uint64_t>::vector;
+    bool HasDot(const Dot& d) const {  // crdt-misc.go:28-34
+        if (size() < d.actor) return false;
+        if (d.actor == size()) throw Error(CRDT_E_ACTOR_RANGE, "HasDot");
+        return (*this)[d.actor] >= d.counter;
+    }
+    uint64_t Counter(Actor a) const {  // crdt-misc.go:36-41
+        if (size() < a) return 0;
+        if (a == size()) throw Error(CRDT_E_ACTOR_RANGE, "Counter");
+        return (*this)[a];
+    }
+    void Merge(const VersionVector& src) {  // crdt-misc.go:43-55
+        for (size_t i = 0; i < src.size(); ++i) {
+            if (i < size()) {
+                if ((*this)[i] < src[i]) (*this)[i] = src[i];
+            } else {
+                push_back(src[i]);
+            }
+        }
+    }
+    VersionVector Clone() const { return *this; }
+    std::string String() const {  // crdt-misc.go:57-68
+        std::string s = "[";
+        for (size_t i = 0; i < size(); ++i) {
+            if (i) s += ", ";
+            s += "(" + std::string(1, char('A' + i)) + " " + std::to_string((*this)[i]) + ")";
+        }
+        return s + "]";
+    }
+};
+
+using Entries = std::unordered_map<std::string, Dot>;
+
+// One context per host thread (crdt_ctx).
+class Engine {
+   public:
+    explicit Engine(int device = 0) { check(crdt_ctx_create(device, &ctx_), "crdt_ctx_create"); }
+    ~Engine() { crdt_ctx_destroy(ctx_); }
+    Engine(const Engine&) = delete;
+    Engine& operator=(const Engine&) = delete;
+    crdt_ctx* ctx() const { return ctx_; }
+    static Engine& Default() {
+        static thread_local Engine e(0);
+        return e;
+    }
+
+   private:
+    crdt_ctx* ctx_ = nullptr;
+};
+
+class AWSetDelta;
+
+// awset.go:55-59
+class AWSet {
+   public:
+    Actor actor = 0;
+    VersionVector versionVector;
+    Entries entries;
+
+    AWSet() = default;
+    AWSet(Actor a, VersionVector vv) : actor(a), versionVector(std::move(vv)) {}
+    virtual ~AWSet() = default;
+
+    std::vector<std::string> SortedValues() const {  // awset.go:61-70
+        std::vector<std::string> v;
+        v.reserve(entries.size());
+        for (auto& kv : entries) v.push_back(kv.first);
+        std::sort(v.begin(), v.end());
+        return v;
+    }
+    void Reset() {  // awset.go:72-75
+        versionVector = VersionVector{0};
+        entries.clear();
+    }
+    AWSet Clone() const { return *this; }                                     // awset.go:77-85
+    bool Has(const std::string& k) const { return entries.count(k) != 0; }    // awset.go:87
+    void Add(std::initializer_list<std::string> keys) {                       // awset.go:89-94
+        for (auto& k : keys) {
+            if (actor >= versionVector.size()) throw Error(CRDT_E_ACTOR_RANGE, "Add");
+            versionVector[actor]++;
+            entries[k] = Dot{actor, versionVector[actor]};
+        }
+    }
+    void Del(std::initializer_list<std::string> keys) {  // awset.go:96-101 (no clock bump)
+        for (auto& k : keys) entries.erase(k);
+    }
+    void Merge(const AWSet& src, Engine& e = Engine::Default());  // awset.go:103-105, on the GPU
+    std::string String() const {                                    // awset.go:163-171
+        std::string s = versionVector.String();
+        for (auto& v : SortedValues()) s += "\n  " + entries.at(v).String() + "  \"" + v + "\"";
+        return s;
+    }
+    virtual const Entries* deleted_map() const { return nullptr; }
+};
+
+// awset-delta_test.go:9-12
+class AWSetDelta : public AWSet {
+   public:
+    Entries deleted;
+
+    AWSetDelta() = default;
+    AWSetDelta(Actor a, VersionVector vv) : AWSet(a, std::move(vv)) {}
+    void Del(std::initializer_list<std::string> keys) {  // awset-delta_test.go:14-33
+        if (actor >= versionVector.size()) throw Error(CRDT_E_ACTOR_RANGE, "Del");
+        versionVector[actor]++;
+        const Dot dot2{actor, versionVector[actor]};
+        for (auto& k : keys) {
+            auto it = entries.find(k);
+            if (it != entries.end()) {
+                deleted[k] = dot2;
+                entries.erase(it);
+            }
+        }
+    }
+    AWSetDelta Clone() const { return *this; }                        // awset-delta_test.go:35-49
+    void Merge(const AWSetDelta& src, Engine& e = Engine::Default());  // awset-delta_test.go:51-65, on the GPU
+    void gcDeleted(const VersionVector&) {}                            // awset-delta_test.go:67-77: empty
+    const Entries* deleted_map() const override { return &deleted; }
+};
+
+namespace detail {
+
+struct Packed {
+    std::vector<uint32_t> offsets{0};
+    std::vector<uint64_t> keys;
+    std::vector<uint32_t> actors;
+    std::vector<uint64_t> counters;
+    std::vector<uint64_t> vv;
+};
+
+inline void pack_entries(const Entries& m, const std::map<std::string, uint64_t>& id, std::vector<uint64_t>& k,
+                         std::vector<uint32_t>& a, std::vector<uint64_t>& c) {
+    std::vector<std::pair<uint64_t, Dot>> v;
+    v.reserve(m.size());
+    for (auto& kv : m) v.emplace_back(id.at(kv.first), kv.second);
+    std::sort(v.begin(), v.end(), [](auto& x, auto& y) { return x.first < y.first; });
+    for (auto& e : v) {
+        k.push_back(e.first);
+        a.push_back(e.second.actor);
+        c.push_back(e.second.counter);
+    }
+}
+
+inline void pack_vv(const VersionVector& v, size_t R, std::vector<uint64_t>& out) {
+    for (size_t r = 0; r < R; ++r) out.push_back(r < v.size() ? v[r] : 0);
+}
+
+template <typename T>
+T* data_or_null(std::vector<T>& v) {
+    return v.empty() ? nullptr : v.data();
+}
+
+// Interning + packing shared by the batch entry points.
+struct Batch {
+    std::map<std::string, uint64_t> id;
+    std::vector<const std::string*> name;
+    size_t R = 1;
+
+    void scan(const AWSet& s) {
+        for (auto& kv : s.entries) id.emplace(kv.first, 0);
+        if (auto* d = s.deleted_map())
+            for (auto& kv : *d) id.emplace(kv.first, 0);
+        R = std::max(R, s.versionVector.size());
+    }
+    void finish() {
+        if (R > CRDT_MAX_R) throw Error(CRDT_E_INVALID, "version vector longer than CRDT_MAX_R");
+        uint64_t i = 0;
+        name.resize(id.size());
+        for (auto& kv : id) {
+            kv.second = i;
+            name[i++] = &kv.first;
+        }
+    }
+    Packed pack(const std::vector<AWSet*>& states) const {
+        Packed p;
+        for (auto* s : states) {
+            pack_entries(s->entries, id, p.keys, p.actors, p.counters);
+            p.offsets.push_back((uint32_t)p.keys.size());
+            pack_vv(s->versionVector, R, p.vv);
+        }
+        return p;
+    }
+    crdt_awset_batch view(Packed& p) const {
+        return crdt_awset_batch{(uint32_t)(p.offsets.size() - 1), (uint32_t)R, p.offsets.data(), nullptr,
+                                data_or_null(p.keys), data_or_null(p.actors), data_or_null(p.counters),
+                                data_or_null(p.vv)};
+    }
+    void unpack(const std::vector<AWSet*>& dsts, const Packed& out, const std::vector<uint32_t>& counts,
+                const std::vector<size_t>& widths) const {
+        for (size_t d = 0; d < dsts.size(); ++d) {
+            Entries m;
+            m.reserve(counts[d]);
+            for (uint32_t j = out.offsets[d]; j < out.offsets[d] + counts[d]; ++j)
+                m[*name[out.keys[j]]] = Dot{out.actors[j], out.counters[j]};
+            dsts[d]->entries = std::move(m);
+            VersionVector vv(widths[d]);
+            for (size_t r = 0; r < widths[d]; ++r) vv[r] = out.vv[d * R + r];
+            dsts[d]->versionVector = std::move(vv);
+        }
+    }
+};
+
+inline Packed make_out(size_t n_docs, size_t R, size_t slots, std::vector<uint32_t>& counts, crdt_awset_out& o) {
+    Packed p;
+    p.offsets.assign(n_docs + 1, 0);
+    p.keys.assign(slots + 1, 0);
+    p.actors.assign(slots + 1, 0);
+    p.counters.assign(slots + 1, 0);
+    p.vv.assign(std::max<size_t>(n_docs * R, 1), 0);
+    counts.assign(std::max<size_t>(n_docs, 1), 0);
+    o = crdt_awset_out{p.offsets.data(), counts.data(), p.keys.data(), p.actors.data(), p.counters.data(), p.vv.data()};
+    return p;
+}
+
+}  // namespace detail
+
+// dsts[i].Merge(*srcs[i]) for every i, as one batched GPU join.
+inline void MergeBatch(const std::vector<AWSet*>& dsts, const std::vector<const AWSet*>& srcs,
+                       Engine& e = Engine::Default()) {
+    if (dsts.size() != srcs.size()) throw Error(CRDT_E_INVALID, "MergeBatch: length mismatch");
+    if (dsts.empty()) return;
+    detail::Batch b;
+    for (auto* s : dsts) b.scan(*s);
+    for (auto* s : srcs) b.scan(*s);
+    b.finish();
+    std::vector<AWSet*> sv;
+    for (auto* s : srcs) sv.push_back(const_cast<AWSet*>(s));
+    detail::Packed pd = b.pack(dsts), ps = b.pack(sv);
+    crdt_awset_batch cd = b.view(pd), cs = b.view(ps);
+    std::vector<uint32_t> counts;
+    crdt_awset_out co;
+    detail::Packed po = detail::make_out(dsts.size(), b.R, pd.keys.size() + ps.keys.size(), counts, co);
+    check(crdt_awset_join_batch(e.ctx(), &cd, &cs, &co), "crdt_awset_join_batch");
+    std::vector<size_t> widths;
+    for (size_t i = 0; i < dsts.size(); ++i)
+        widths.push_back(std::max(dsts[i]->versionVector.size(), srcs[i]->versionVector.size()));
+    b.unpack(dsts, po, counts, widths);
+}
+
+namespace detail {
+inline void fold(int mode, const std::vector<AWSet*>& dsts, const std::vector<std::vector<const AWSet*>>& srcs,
+                 Engine& e) {
+    if (dsts.size() != srcs.size()) throw Error(CRDT_E_INVALID, "fold: length mismatch");
+    if (dsts.empty()) return;
+    Batch b;
+    for (auto* s : dsts) b.scan(*s);
+    for (auto& l : srcs)
+        for (auto* s : l) b.scan(*s);
+    b.finish();
+    Packed pd = b.pack(dsts);
+    std::vector<uint32_t> doc_srcs{0}, src_actor, entry_off{0}, tomb_off{0};
+    std::vector<uint64_t> vv, keys, counters, tkeys, tcounters;
+    std::vector<uint32_t> actors, tactors;
+    for (auto& l : srcs) {
+        for (auto* s : l) {
+            src_actor.push_back(s->actor);
+            pack_vv(s->versionVector, b.R, vv);
+            pack_entries(s->entries, b.id, keys, actors, counters);
+            entry_off.push_back((uint32_t)keys.size());
+            if (auto* del = s->deleted_map()) pack_entries(*del, b.id, tkeys, tactors, tcounters);
+            tomb_off.push_back((uint32_t)tkeys.size());
+        }
+        doc_srcs.push_back((uint32_t)src_actor.size());
+    }
+    crdt_awset_batch cd = b.view(pd);
+    crdt_src_batch cs{(uint32_t)dsts.size(), (uint32_t)b.R, doc_srcs.data(), data_or_null(src_actor),
+                      data_or_null(vv), entry_off.data(), data_or_null(keys), data_or_null(actors),
+                      data_or_null(counters), tomb_off.data(), data_or_null(tkeys), data_or_null(tactors),
+                      data_or_null(tcounters)};
+    std::vector<uint32_t> counts;
+    crdt_awset_out co;
+    Packed po = make_out(dsts.size(), b.R, pd.keys.size() + keys.size(), counts, co);
+    check(crdt_awset_fold_batch(e.ctx(), mode, &cd, &cs, &co), "crdt_awset_fold_batch");
+    std::vector<size_t> widths;
+    for (size_t i = 0; i < dsts.size(); ++i) {
+        size_t w = dsts[i]->versionVector.size();
+        for (auto* s : srcs[i]) w = std::max(w, s->versionVector.size());
+        widths.push_back(w);
+    }
+    b.unpack(dsts, po, counts, widths);
+}
+}  // namespace detail
+
+// for each i, for src in srcs[i] in order: dsts[i]->Merge(*src)  (AWSet semantics)
+inline void FoldBatch(const std::vector<AWSet*>& dsts, const std::vector<std::vector<const AWSet*>>& srcs,
+                      Engine& e = Engine::Default()) {
+    detail::fold(CRDT_FOLD_AWSET, dsts, srcs, e);
+}
+
+// for each i, for src in srcs[i] in order: dsts[i]->Merge(*src)  (AWSetDelta semantics)
+inline void DeltaMergeBatch(const std::vector<AWSetDelta*>& dsts,
+                            const std::vector<std::vector<const AWSetDelta*>>& srcs, Engine& e = Engine::Default()) {
+    std::vector<AWSet*> d(dsts.begin(), dsts.end());
+    std::vector<std::vector<const AWSet*>> s;
+    for (auto& l : srcs) s.emplace_back(l.begin(), l.end());
+    detail::fold(CRDT_FOLD_DELTA, d, s, e);
+}
+
+inline void AWSet::Merge(const AWSet& src, Engine& e) { MergeBatch({this}, {&src}, e); }
+inline void AWSetDelta::Merge(const AWSetDelta& src, Engine& e) { DeltaMergeBatch({this}, {{&src}}, e); }
+
+}  // namespace crdt
