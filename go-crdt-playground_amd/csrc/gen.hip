@@ -247,10 +247,13 @@ __global__ __launch_bounds__(WAVES * 64) void gen_replicas_kernel(uint64_t seed,
             const uint32_t slot = popc(m & low_mask(lane));
             const uint64_t he = Hx(seed, d, 22, r * 64 + u);
             uint32_t a = (he & 3) == 0 ? (uint32_t)((he >> 2) % R) : r;
-            uint64_t va = __shfl(vv, (int)a);
-            if (va == 0) {  // never seen that actor: fall back to own dot
+            // both shuffles run in every lane (a shuffle inside a divergent branch
+            // reads inactive source lanes)
+            const uint64_t va_a = __shfl(vv, (int)a), va_r = __shfl(vv, (int)r);
+            uint64_t va = va_a;
+            if (va_a == 0) {  // never seen that actor: fall back to own dot
                 a = r;
-                va = __shfl(vv, (int)r);
+                va = va_r;
             }
             const uint64_t c = 1 + (he >> 16) % va;
             const uint64_t key = ((uint64_t)d << 8) | u;

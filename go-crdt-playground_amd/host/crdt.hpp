@@ -316,10 +316,11 @@ inline void fold(int mode, const std::vector<AWSet*>& dsts, const std::vector<st
         doc_srcs.push_back((uint32_t)src_actor.size());
     }
     crdt_awset_batch cd = b.view(pd);
+    const bool tombs = !tkeys.empty();  // no tombstones at all: tomb_off = NULL
     crdt_src_batch cs{(uint32_t)dsts.size(), (uint32_t)b.R, doc_srcs.data(), data_or_null(src_actor),
                       data_or_null(vv), entry_off.data(), data_or_null(keys), data_or_null(actors),
-                      data_or_null(counters), tomb_off.data(), data_or_null(tkeys), data_or_null(tactors),
-                      data_or_null(tcounters)};
+                      data_or_null(counters), tombs ? tomb_off.data() : nullptr, data_or_null(tkeys),
+                      data_or_null(tactors), data_or_null(tcounters)};
     std::vector<uint32_t> counts;
     crdt_awset_out co;
     Packed po = make_out(dsts.size(), b.R, pd.keys.size() + keys.size(), counts, co);
