@@ -127,6 +127,22 @@ __device__ __forceinline__ uint32_t lower_bound_pow(const uint64_t* a, uint32_t 
     return pos;
 }
 
+// As lower_bound_pow, but probes only the steps that fit n (n wave-uniform:
+// the skipped steps are scalar branches), so short lists cost few LDS reads.
+template <int LOG>
+__device__ __forceinline__ uint32_t lower_bound_adapt(const uint64_t* a, uint32_t n, uint64_t key) {
+    uint32_t pos = 0;
+#pragma unroll
+    for (int s = LOG; s >= 0; --s) {
+        const uint32_t step = 1u << s;
+        if (step > n) continue;
+        const bool in = pos + step <= n;
+        const uint64_t v = a[in ? pos + step - 1 : 0u];
+        pos += (in && v < key) ? step : 0u;
+    }
+    return pos;
+}
+
 // Generic lower bound for any n (global or LDS memory).
 __device__ __forceinline__ uint32_t lower_bound(const uint64_t* a, uint32_t n, uint64_t key) {
     uint32_t lo = 0, hi = n;

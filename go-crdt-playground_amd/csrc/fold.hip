@@ -22,121 +22,178 @@
 
 namespace crdt {
 
+// LDS of one wavefront: the document (two ping-pong buffers of CAP slots) and
+// ALL of its sources (entries, tombstones, version vectors), loaded in one
+// burst so that no fold step waits on HBM.
 template <int CAP>
 struct FoldWaveSmem {
+    static constexpr int SCAP = 128;  // Σ source entries of a doc
+    static constexpr int TCAP = 64;   // Σ tombstones of a doc
+    static constexpr int VCAP = 256;  // Σ source VV words (sources x R)
+    static constexpr int MCAP = 64;   // sources per doc
     uint64_t bk[2][CAP];
     uint64_t bc[2][CAP];
     uint32_t ba[2][CAP];
-    uint32_t kp[CAP + 1];
-    uint64_t sk[64];
-    uint64_t sc[64];
-    uint64_t tk[64];
-    uint64_t tc[64];
-    uint32_t sa[64];
-    uint32_t ta[64];
-    uint32_t teff[64];
+    uint32_t kp[CAP + 1];   // exclusive prefix of surviving document entries
+    uint32_t mark[CAP];     // doc slot -> (src lane + 1) that owns it this step
+    uint32_t tmark[CAP];    // doc slot -> (tombstone lane + 1) that hits it
+    uint32_t stomb[64];     // src lane -> (tombstone lane + 1) on the same key
+    uint64_t sk[SCAP];
+    uint64_t sc[SCAP];
+    uint32_t sa[SCAP];
+    uint64_t tk[TCAP];
+    uint64_t tc[TCAP];
+    uint32_t ta[TCAP];
+    uint64_t svv[VCAP];
+    uint32_t soff[MCAP + 1];  // source j: entries [soff[j], soff[j+1]) relative to the doc
+    uint32_t toff[MCAP + 1];
+    uint32_t sact[MCAP];
     uint64_t dvv[CRDT_MAX_R];
-    uint64_t svv[CRDT_MAX_R];
 };
+
+// Burst-load n_elems 8/4/8-byte entry triples starting at o into LDS (lanes
+// stride 64; unconditional buffer loads, out-of-range lanes read 0).
+template <int CHUNKS>
+__device__ __forceinline__ void burst_entries(uint64_t* k, uint32_t* a, uint64_t* c, const uint64_t* gk,
+                                              const uint32_t* ga, const uint64_t* gc, uint32_t o, uint32_t n,
+                                              uint32_t lane) {
+    const rsrc_t rk = make_rsrc(gk + o, n * 8u), ra = make_rsrc(ga + o, n * 4u), rc = make_rsrc(gc + o, n * 8u);
+    uint64_t kk[CHUNKS], cc[CHUNKS];
+    uint32_t aa[CHUNKS];
+#pragma unroll
+    for (int q = 0; q < CHUNKS; ++q) {
+        const uint32_t i = q * 64 + lane;
+        kk[q] = ld64(rk, i * 8u);
+        aa[q] = ld32(ra, i * 4u);
+        cc[q] = ld64(rc, i * 8u);
+    }
+#pragma unroll
+    for (int q = 0; q < CHUNKS; ++q) {
+        const uint32_t i = q * 64 + lane;
+        k[i] = kk[q];
+        a[i] = aa[q];
+        c[i] = cc[q];
+    }
+}
 
 template <int WAVES, int CAP, int LOGCAP>
 __global__ __launch_bounds__(WAVES * 64) void fold_wave_kernel(int mode, BatchView dst, SrcView sb, OutView out,
                                                                  Work wk) {
-    __shared__ FoldWaveSmem<CAP> smem[WAVES];
+    using Smem = FoldWaveSmem<CAP>;
+    __shared__ Smem smem[WAVES];
     constexpr int NCH = CAP / 64;
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t w = threadIdx.x >> 6;
-    FoldWaveSmem<CAP>& m = smem[w];
+    Smem& m = smem[w];
     const uint32_t R = dst.R;
     const uint32_t n_docs = dst.n_docs;
     const uint64_t lt = low_mask(lane);
+    const bool delta = mode == CRDT_FOLD_DELTA;
     uint32_t err = 0;
 
     for (uint32_t d0 = blockIdx.x * WAVES + w; d0 < n_docs; d0 += gridDim.x * WAVES) {
         const uint32_t d = uniform(d0);
         const uint32_t s0 = sb.doc_srcs[d], s1 = sb.doc_srcs[d + 1];
+        const uint32_t ms = s1 - s0;
         const uint32_t doff = dst.offsets[d];
-        const uint32_t obase = doff + sb.entry_off[s0];
+        const uint32_t e0 = sb.entry_off[s0], E = sb.entry_off[s1] - e0;
+        const uint32_t t0 = (sb.tomb_off && delta) ? sb.tomb_off[s0] : 0u;
+        const uint32_t X = (sb.tomb_off && delta) ? sb.tomb_off[s1] - t0 : 0u;
+        const uint32_t obase = doff + e0;
         uint32_t n = live_count(dst.offsets, dst.counts, d);
         if (lane == 0) {
             out.offsets[d] = obase;
             if (d == n_docs - 1) out.offsets[n_docs] = dst.offsets[n_docs] + sb.entry_off[sb.doc_srcs[n_docs]];
         }
-        // eligibility for the wave path
-        bool bad = n > CAP;
-        for (uint32_t k = s0 + lane; k < s1; k += 64) {
-            const uint32_t c = sb.entry_off[k + 1] - sb.entry_off[k];
-            const uint32_t x = sb.tomb_off ? sb.tomb_off[k + 1] - sb.tomb_off[k] : 0u;
-            bad |= (c > 64) || (x > 64);
+        // eligibility for the LDS path (else: block path, nothing written yet)
+        bool bad = n > CAP || E > Smem::SCAP || X > Smem::TCAP || ms > Smem::MCAP || ms * R > Smem::VCAP;
+        if (!bad) {
+            const uint32_t k = s0 + lane;
+            const uint32_t c = lane < ms ? sb.entry_off[k + 1] - sb.entry_off[k] : 0u;
+            const uint32_t x = (lane < ms && X) ? sb.tomb_off[k + 1] - sb.tomb_off[k] : 0u;
+            bad = ballot(c > 64 || x > 64) != 0;
         }
-        if (ballot(bad)) {
+        if (bad) {
             if (lane == 0) wk.worklist[atomicAdd(wk.wl_count, 1u)] = d;
             continue;
         }
-        for (uint32_t i = lane; i < n; i += 64) {
-            m.bk[0][i] = dst.keys[doff + i];
-            m.ba[0][i] = dst.actors[doff + i];
-            m.bc[0][i] = dst.counters[doff + i];
+        // ---- one burst: document, source entries, tombstones, VVs, actors, offsets
+        burst_entries<NCH>(m.bk[0], m.ba[0], m.bc[0], dst.keys, dst.actors, dst.counters, doff, n, lane);
+        burst_entries<Smem::SCAP / 64>(m.sk, m.sa, m.sc, sb.keys, sb.actors, sb.counters, e0, E, lane);
+        if (delta) burst_entries<Smem::TCAP / 64>(m.tk, m.ta, m.tc, sb.tkeys, sb.tactors, sb.tcounters, t0, X, lane);
+        {
+            const rsrc_t rv = make_rsrc(sb.vv + (size_t)s0 * R, ms * R * 8u);
+            uint64_t vq[Smem::VCAP / 64];
+#pragma unroll
+            for (int q = 0; q < Smem::VCAP / 64; ++q) vq[q] = ld64(rv, (q * 64 + lane) * 8u);
+            const uint32_t eo = ld32(make_rsrc(sb.entry_off + s0, (ms + 1) * 4u), lane * 4u);
+            const uint32_t eo2 = ld32(make_rsrc(sb.entry_off + s0, (ms + 1) * 4u), (64 + lane) * 4u);
+            const uint32_t to = X ? ld32(make_rsrc(sb.tomb_off + s0, (ms + 1) * 4u), lane * 4u) : 0u;
+            const uint32_t to2 = X ? ld32(make_rsrc(sb.tomb_off + s0, (ms + 1) * 4u), (64 + lane) * 4u) : 0u;
+            const uint32_t ac = ld32(make_rsrc(sb.src_actor + s0, ms * 4u), lane * 4u);
+            const uint64_t dv = ld64(make_rsrc(dst.vv + (size_t)d * R, R * 8u), lane * 8u);
+#pragma unroll
+            for (int q = 0; q < Smem::VCAP / 64; ++q) m.svv[q * 64 + lane] = vq[q];
+            m.soff[lane] = eo - e0;
+            if (lane == 0) m.soff[64] = eo2 - e0;
+            m.toff[lane] = to - t0;
+            if (lane == 0) m.toff[64] = to2 - t0;
+            m.sact[lane] = ac;
+            m.dvv[lane] = dv;
         }
-        if (lane < R) m.dvv[lane] = dst.vv[(size_t)d * R + lane];
+        m.stomb[lane] = 0;
+#pragma unroll
+        for (int q = 0; q < NCH; ++q) {
+            m.mark[q * 64 + lane] = 0;
+            m.tmark[q * 64 + lane] = 0;
+        }
+        wave_sync();
+
         uint32_t cur = 0;
         bool bailed = false;
-
-        for (uint32_t k = s0; k < s1; ++k) {
-            const uint32_t e0 = sb.entry_off[k];
-            const uint32_t c = sb.entry_off[k + 1] - e0;
-            const uint32_t t0 = sb.tomb_off ? sb.tomb_off[k] : 0u;
-            const uint32_t x = sb.tomb_off ? sb.tomb_off[k + 1] - t0 : 0u;
-            const bool sv = lane < c, tv = lane < x;
-            uint64_t skey = 0, scnt = 0;
-            uint32_t sact = 0;
-            if (sv) {
-                skey = sb.keys[e0 + lane];
-                sact = sb.actors[e0 + lane];
-                scnt = sb.counters[e0 + lane];
-            }
-            m.sk[lane] = skey;
-            m.sa[lane] = sact;
-            m.sc[lane] = scnt;
-            uint64_t tkey = 0, tcnt = 0;
-            uint32_t tact = 0;
-            if (tv && mode == CRDT_FOLD_DELTA) {
-                tkey = sb.tkeys[t0 + lane];
-                tact = sb.tactors[t0 + lane];
-                tcnt = sb.tcounters[t0 + lane];
-            }
-            m.tk[lane] = tkey;
-            m.ta[lane] = tact;
-            m.tc[lane] = tcnt;
-            if (lane < R) m.svv[lane] = sb.vv[(size_t)k * R + lane];
-            wave_sync();
+        for (uint32_t j = 0; j < ms; ++j) {
+            const uint32_t ej = m.soff[j], c = m.soff[j + 1] - ej;
+            const uint32_t tj = delta ? m.toff[j] : 0u;
+            const uint64_t* svv = m.svv + j * R;
+            const bool sv = lane < c;
+            const uint64_t skey = sv ? m.sk[ej + lane] : 0ull;
+            const uint32_t sact = sv ? m.sa[ej + lane] : 0u;
+            const uint64_t scnt = sv ? m.sc[ej + lane] : 0ull;
 
             // path select (awset-delta_test.go:53)
             uint32_t perr = 0;
-            const bool full = (mode != CRDT_FOLD_DELTA) || vv_counter(m.dvv, R, sb.src_actor[k], perr) == 0;
+            const bool full = !delta || vv_counter(m.dvv, R, m.sact[j], perr) == 0;
             err |= perr;
-            if (perr) {  // the reference panics here; stop this document
-                wave_sync();
-                break;
-            }
-            const uint32_t xd = full ? 0u : x;  // tombstones matter only on the delta path
+            if (perr) break;  // the reference panics here; outputs undefined
+            const uint32_t x = full ? 0u : m.toff[j + 1] - tj;  // tombstones matter only on the delta path
+            const bool tv = lane < x;
+            const uint64_t tkey = tv ? m.tk[tj + lane] : 0ull;
+            const uint32_t tact = tv ? m.ta[tj + lane] : 0u;
+            const uint64_t tcnt = tv ? m.tc[tj + lane] : 0ull;
 
-            // src entry lanes: position in the document, "changed" (dot pruning)
-            const uint32_t f = lower_bound_pow<LOGCAP>(m.bk[cur], n, skey);
-            const bool in_d = sv && f < n && m.bk[cur][f] == skey;
+            // searches: src key in the doc; tombstone key in the doc and in src
+            const uint32_t f = lower_bound_adapt<LOGCAP>(m.bk[cur], n, skey);
+            const bool in_d = sv && f < n && m.bk[cur][f < CAP ? f : 0] == skey;
             const bool changed = sv && (full || !has_dot(m.dvv, R, sact, scnt, err));
-            // tombstone lanes: effective unless re-added (awset-delta_test.go:93-102)
-            bool eff = false;
-            if (lane < xd) {
-                const uint32_t g = lower_bound_pow<6>(m.sk, c, tkey);
-                const bool in_s = g < c && m.sk[g] == tkey;
-                eff = !(in_s && (m.sa[g] != tact || m.sc[g] > tcnt));
+            bool eff = false, t_in_d = false;
+            uint32_t g = 0, q = 0;
+            if (x) {
+                g = lower_bound_adapt<6>(m.sk + ej, c, tkey);
+                q = lower_bound_adapt<LOGCAP>(m.bk[cur], n, tkey);
+                const bool in_s = tv && g < c && m.sk[ej + (g & 63)] == tkey;
+                t_in_d = tv && q < n && m.bk[cur][q < CAP ? q : 0] == tkey;
+                // awset-delta_test.go:93-102: a tombstone re-added since is dropped
+                eff = tv && !(in_s && (m.sa[ej + (g & 63)] != tact || m.sc[ej + (g & 63)] > tcnt));
+                if (eff && in_s) m.stomb[g & 63] = lane + 1;
+                if (eff && t_in_d) m.tmark[q] = lane + 1;
             }
-            m.teff[lane] = eff ? 1u : 0u;
             if (!full && !ballot(changed) && !ballot(eff)) {  // :60 no-op, VV untouched
                 wave_sync();
+                if (eff && t_in_d) m.tmark[q] = 0;
+                if (eff && g < 64) m.stomb[g & 63] = 0;
                 continue;
             }
+            if (in_d) m.mark[f] = lane + 1;
             wave_sync();
 
             // decisions for src lanes (they own every key present in src)
@@ -153,10 +210,8 @@ __global__ __launch_bounds__(WAVES * 64) void fold_wave_kernel(int mode, BatchVi
                 } else {
                     pres_s = changed && !has_dot(m.dvv, R, sact, scnt, err);
                 }
-                if (pres_s && xd) {
-                    const uint32_t h = lower_bound_pow<6>(m.tk, xd, skey);
-                    if (h < xd && m.tk[h] == skey && m.teff[h]) pres_s = has_dot(m.dvv, R, m.ta[h], m.tc[h], err);
-                }
+                const uint32_t h = m.stomb[lane];
+                if (pres_s && h) pres_s = has_dot(m.dvv, R, m.ta[tj + h - 1], m.tc[tj + h - 1], err);
             }
             const uint64_t emit_s = ballot(pres_s);
 
@@ -165,24 +220,22 @@ __global__ __launch_bounds__(WAVES * 64) void fold_wave_kernel(int mode, BatchVi
             uint32_t g_d[NCH];
             uint32_t carry = 0;
 #pragma unroll
-            for (int q = 0; q < NCH; ++q) {
-                const uint32_t idx = q * 64 + lane;
+            for (int qq = 0; qq < NCH; ++qq) {
+                const uint32_t idx = qq * 64 + lane;
                 const bool valid = idx < n;
-                const uint64_t key = valid ? m.bk[cur][idx] : 0ull;
-                const uint32_t g = lower_bound_pow<6>(m.sk, c, key);
-                const bool in_s = valid && g < c && m.sk[g] == key;
+                const uint64_t key = m.bk[cur][idx];
+                const bool owned = m.mark[idx] != 0;
+                const uint32_t th = m.tmark[idx];
                 bool pres = false;
-                if (valid && !in_s) {
-                    pres = full ? !has_dot(m.svv, R, m.ba[cur][idx], m.bc[cur][idx], err) : true;
-                    if (pres && xd) {
-                        const uint32_t h = lower_bound_pow<6>(m.tk, xd, key);
-                        if (h < xd && m.tk[h] == key && m.teff[h]) pres = has_dot(m.dvv, R, m.ta[h], m.tc[h], err);
-                    }
+                if (valid && !owned) {
+                    pres = full ? !has_dot(svv, R, m.ba[cur][idx], m.bc[cur][idx], err) : true;
+                    if (pres && th) pres = has_dot(m.dvv, R, m.ta[tj + th - 1], m.tc[tj + th - 1], err);
                 }
+                // # src keys < key (its shift by inserted src entries)
+                g_d[qq] = lower_bound_adapt<6>(m.sk + ej, c, key);
                 const uint64_t bm = ballot(pres);
                 if (valid) m.kp[idx] = carry + popc(bm & lt);
-                emit_d[q] = pres;
-                g_d[q] = g;
+                emit_d[qq] = pres;
                 carry += popc(bm);
             }
             if (lane == 0) m.kp[n] = carry;
@@ -200,16 +253,20 @@ __global__ __launch_bounds__(WAVES * 64) void fold_wave_kernel(int mode, BatchVi
                 m.bc[nx][pos] = oc_s;
             }
 #pragma unroll
-            for (int q = 0; q < NCH; ++q) {
-                if (emit_d[q]) {
-                    const uint32_t idx = q * 64 + lane;
-                    const uint32_t pos = m.kp[idx] + popc(emit_s & low_mask(g_d[q]));
+            for (int qq = 0; qq < NCH; ++qq) {
+                if (emit_d[qq]) {
+                    const uint32_t idx = qq * 64 + lane;
+                    const uint32_t pos = m.kp[idx] + popc(emit_s & low_mask(g_d[qq]));
                     m.bk[nx][pos] = m.bk[cur][idx];
                     m.ba[nx][pos] = m.ba[cur][idx];
                     m.bc[nx][pos] = m.bc[cur][idx];
                 }
             }
-            if (lane < R) m.dvv[lane] = max(m.dvv[lane], m.svv[lane]);
+            // clear this step's marks
+            if (in_d) m.mark[f] = 0;
+            if (eff && t_in_d) m.tmark[q] = 0;
+            if (eff && g < 64) m.stomb[g & 63] = 0;
+            if (lane < R) m.dvv[lane] = max(m.dvv[lane], svv[lane]);
             n = new_n;
             cur = nx;
             wave_sync();
@@ -219,10 +276,14 @@ __global__ __launch_bounds__(WAVES * 64) void fold_wave_kernel(int mode, BatchVi
             wave_sync();
             continue;
         }
-        for (uint32_t i = lane; i < n; i += 64) {
-            out.keys[obase + i] = m.bk[cur][i];
-            out.actors[obase + i] = m.ba[cur][i];
-            out.counters[obase + i] = m.bc[cur][i];
+        const rsrc_t ok = make_rsrc(out.keys + obase, n * 8u), oa = make_rsrc(out.actors + obase, n * 4u),
+                     oc = make_rsrc(out.counters + obase, n * 8u);
+#pragma unroll
+        for (int qq = 0; qq < NCH; ++qq) {
+            const uint32_t i = qq * 64 + lane;
+            st64<kAuxNT>(m.bk[cur][i], ok, i * 8u);
+            st32<kAuxNT>(m.ba[cur][i], oa, i * 4u);
+            st64<kAuxNT>(m.bc[cur][i], oc, i * 8u);
         }
         if (lane == 0) out.counts[d] = n;
         if (lane < R) out.vv[(size_t)d * R + lane] = m.dvv[lane];
@@ -311,7 +372,7 @@ __global__ __launch_bounds__(NT) void fold_block_kernel(int mode, BatchView dst,
     if (__syncthreads_or(err != 0) && tid == 0) atomicOr(wk.status, kErrActorRange);
 }
 
-constexpr int kFoldWaves = 4;
+constexpr int kFoldWaves = 2;
 constexpr int kFoldCap = 128;
 constexpr int kFoldLogCap = 7;
 constexpr int kFoldNT = 256;
