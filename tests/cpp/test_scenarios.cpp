@@ -199,7 +199,7 @@ static void TestBatches() {
     s1.Add({"p", "q"});
     s2.Add({"q"});
     FoldBatch({&d}, {{&s1, &s2}});
-    expect(d, {{"p", {1, 1}}, {"q", {2, 1}}}, {0, 1, 1});
+    expect(d, {{"p", {1, 1}}, {"q", {2, 1}}}, {0, 2, 1});
 }
 
 int main() {

@@ -18,6 +18,16 @@ cpass() {
   timeout -k 10 -s KILL 120 rocprofv3 --pmc "$@" --output-format csv -d "$OUT/$name" -o run -- python3 tools/calib.py > "$OUT/$name.log" 2>&1
   local rc=$?; echo "[pmc $name] rc=$rc"; [ $rc -eq 0 ] || { tail -20 "$OUT/$name.log"; exit $rc; }
 }
+if [ "${FOLD:-0}" = 1 ]; then
+  BENCH="python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline ${BENCH_ARGS:-}"
+  pass sq SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU
+  pass lds SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_SALU SQ_INSTS_SMEM SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS GRBM_GUI_ACTIVE GRBM_COUNT
+  pass lds2 SQ_LDS_IDX_ACTIVE SQ_LDS_ADDR_CONFLICT SQ_LDS_UNALIGNED_STALL SQ_INSTS_VMEM SQ_INST_LEVEL_LDS SQ_ACCUM_PREV_HIRES
+  pass fetch FETCH_SIZE
+  pass write WRITE_SIZE
+  python3 tools/traffic.py "$OUT" --docs ${DOCS:-1048576} > "$OUT/summary.txt"; cat "$OUT/summary.txt" | grep -A30 fold_wave
+  exit 0
+fi
 pass fetch FETCH_SIZE
 pass write WRITE_SIZE
 pass sq SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU
