@@ -10,13 +10,15 @@ replica state, R = 2, synthetic reachable states generated on the device
   all-reduced (max, u64) across GPUs over RCCL when N > 1.
 --config 3: delta-state anti-entropy -- 10 ordered AWSetDelta sources folded
   into each of 1,048,576 docs (R = 16): 10,485,760 merges per step.
+--config 4: 16,384 docs with Zipf(1.1)-like sizes up to 2^20 entries, 50%
+  concurrent add/remove conflicts, joined both directions (block path).
 --config 5: 12.5M docs per GPU (100M over 8 GPUs) x 8 replicas of 16 entries
   (R = 8) folded r0 <- r1 <- ... <- r7, plus the global causal context.
 Inputs are resident in HBM before the timed region.  Metric: replica merges/s
 (whole job), with the dominant kernel's achieved algorithmic HBM bandwidth
 against the 8 TB/s roofline and the C oracle timed on the host beside it.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2|3|5]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2|3|4|5]
   torchrun --nproc-per-node N bench.py --gpus N ...   (one process per GPU)
 """
 
@@ -137,6 +139,69 @@ class Config2:
                 "sample": "first %d docs of the config-2 batch, both directions, C oracle (oracle/awset_oracle.c, "
                           "sorted-array restatement of awset.go:107-161), 1 thread, %d merges in %.1f s "
                           "(no Go toolchain on the box: the reference itself cannot run)" % (n_sample, merges, el)}
+
+
+class Config4:
+    """Skewed sizes (Zipf(1.1)-like, up to 2^20 entries) with 50% concurrent
+    add/remove conflicts, full-state join both directions (BASELINE configs[3])."""
+
+    R = 2
+    kernel = "join_block_kernel"
+    metric = "replica-merges/sec (AWSet join, Zipf sizes, config 4) + achieved HBM GB/s (% roofline)"
+
+    def __init__(self, eng, n, seed, dev, stream):
+        import numpy as np
+        import torch
+
+        from crdtgpu.batch import OutBuffers
+        from crdtgpu.engine import zipf_sizes
+
+        self.eng, self.n, self.stream = eng, n, stream
+        R = self.R
+        sizes = zipf_sizes(seed, n)
+        offs = np.zeros(n + 1, dtype=np.uint32)
+        np.cumsum(sizes, out=offs[1:])
+        self.total = int(offs[-1])
+        self.d_offs = torch.from_numpy(offs.view(np.int32).copy()).to(dev)
+        eng.reserve(n, 0)
+        self.A = OutBuffers(n, R, self.total, device=dev)
+        self.B = OutBuffers(n, R, self.total, device=dev)
+        eng.gen_zipf_async(seed, n, self.d_offs, self.A, self.B, stream=stream)
+        self.oab = OutBuffers(n, R, 2 * self.total, device=dev)
+        self.oba = OutBuffers(n, R, 2 * self.total, device=dev)
+        self.ctx_ab = torch.zeros(R, dtype=torch.int64, device=dev)
+        self.ctx_ba = torch.zeros(R, dtype=torch.int64, device=dev)
+        self.a, self.b = self.A.as_batch(), self.B.as_batch()
+        self.merges_per_step = 2 * n
+        self.n_events = 3
+        self.sizes = sizes
+
+    step = Config2.step
+    launch_seconds = Config2.launch_seconds
+    bytes_per_launch = Config2.bytes_per_launch
+
+    def describe(self, world):
+        return {"workload": "config4: %d docs/GPU, Zipf(1.1)-like sizes in [1, 2^20) (mean %.0f, max %d, %d entries "
+                            "per side), 50%% concurrent add/remove conflicts, R=2, full-state join both directions"
+                            % (self.n, self.sizes.mean(), self.sizes.max(), self.total),
+                "docs_per_gpu": self.n, "R": self.R, "entries_per_side": self.total,
+                "merges_per_step": self.merges_per_step * world, "parallelism": "doc-sharded x%d" % world}
+
+    def cpu_baseline(self, n_sample, budget_s):
+        from oracle import oracle
+
+        n_sample = min(n_sample, 256)
+        ha, hb = _host_batch(self.A, n_sample, self.R), _host_batch(self.B, n_sample, self.R)
+
+        def run():
+            rc1, _ = oracle.join(ha, hb)
+            rc2, _ = oracle.join(hb, ha)
+            assert rc1 == 0 and rc2 == 0
+
+        merges, el = _time_cpu(run, 2 * n_sample, budget_s)
+        return {"value": merges / el, "unit": "merges/s", "cores": 1, "kind": "port",
+                "sample": "first %d docs of the config-4 batch (%d entries per side), both directions, C oracle, "
+                          "1 thread, %d merges in %.1f s" % (n_sample, int(ha.offsets[-1]), merges, el)}
 
 
 class Config3:
@@ -306,7 +371,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--config", type=int, default=2, choices=[2, 3, 5])
+    ap.add_argument("--config", type=int, default=2, choices=[2, 3, 4, 5])
     ap.add_argument("--docs", type=int, default=None,
                     help="documents per GPU (default 1,048,576; config 5: 12,500,000 = 100M / 8)")
     ap.add_argument("--seed", type=int, default=0x5EED)
@@ -335,11 +400,11 @@ def main():
     torch.cuda.set_device(dev)
     stream = torch.cuda.current_stream()
 
-    n = args.docs or (12_500_000 if args.config == 5 else 1 << 20)
+    n = args.docs or {5: 12_500_000, 4: 16_384}.get(args.config, 1 << 20)
     eng = crdtgpu.Engine(local)
     # each rank owns its own documents (weak scaling; no data-path exchange)
     seed = args.seed + (rank << 40)
-    W = {2: Config2, 3: Config3, 5: Config5}[args.config](eng, n, seed, dev, stream)
+    W = {2: Config2, 3: Config3, 4: Config4, 5: Config5}[args.config](eng, n, seed, dev, stream)
     eng.sync(stream)
 
     def step(ev=None):

@@ -112,6 +112,8 @@ def _load():
         "crdt_causal_context_async": (ctypes.c_int, [_vp, _vp, _u32, _u32, _vp, _vp]),
         "crdt_gen_pair_async": (ctypes.c_int, [_vp, _u64, _u32, P(CAWSetOut), P(CAWSetOut), _vp]),
         "crdt_gen_delta_async": (ctypes.c_int, [_vp, _u64, _u32, _u32, _u32, P(CAWSetOut), P(CSrcBatch), _vp]),
+        "crdt_gen_zipf_sizes": (ctypes.c_int, [_u64, _u32, _vp]),
+        "crdt_gen_zipf_async": (ctypes.c_int, [_vp, _u64, _u32, _vp, P(CAWSetOut), P(CAWSetOut), _vp]),
         "crdt_gen_replicas_async": (ctypes.c_int, [_vp, _u64, _u32, _u32, _u32, P(CAWSetOut), P(CSrcBatch), _vp]),
         "crdt_awset_join_batch": (ctypes.c_int, [_vp, P(CAWSetBatch), P(CAWSetBatch), P(CAWSetOut)]),
         "crdt_awset_fold_batch": (ctypes.c_int, [_vp, ctypes.c_int, P(CAWSetBatch), P(CSrcBatch), P(CAWSetOut)]),

@@ -90,6 +90,11 @@ class Engine:
         check(self._lib.crdt_gen_replicas_async(self._ctx, int(seed), int(n_docs), int(P), int(E), ctypes.byref(cd),
                                                 ctypes.byref(cs), _stream(stream)), "crdt_gen_replicas_async")
 
+    def gen_zipf_async(self, seed: int, n_docs: int, offsets, a: OutBuffers, b: OutBuffers, stream=None):
+        ca, cb = a.c(), b.c()
+        check(self._lib.crdt_gen_zipf_async(self._ctx, int(seed), int(n_docs), ptr(offsets), ctypes.byref(ca),
+                                            ctypes.byref(cb), _stream(stream)), "crdt_gen_zipf_async")
+
     # -- host buffers, synchronous ----------------------------------------
     def join(self, dst: AWSetBatch, src: AWSetBatch) -> OutBuffers:
         dst, src = dst.numpy(), src.numpy()
@@ -106,6 +111,15 @@ class Engine:
         check(self._lib.crdt_awset_fold_batch(self._ctx, int(mode), ctypes.byref(d), ctypes.byref(s),
                                               ctypes.byref(o)), "crdt_awset_fold_batch")
         return out
+
+
+def zipf_sizes(seed: int, n_docs: int):
+    """Document sizes of the "zipf" workload (host computation, no GPU)."""
+    import numpy as np
+
+    out = np.zeros(max(n_docs, 1), dtype=np.uint32)
+    check(abi.lib().crdt_gen_zipf_sizes(int(seed), int(n_docs), out.ctypes.data), "crdt_gen_zipf_sizes")
+    return out[:n_docs]
 
 
 def validate(batch: AWSetBatch) -> int:

@@ -138,6 +138,56 @@ def replica_docs(seed: int, docs, P: int = 8, E: int = 16):
     return dsts, srcs
 
 
+ZIPF_W = [65536, 61147, 57052, 53232, 49667, 46341, 43238, 40342, 37641, 35120,
+          32768, 30574, 28526, 26616, 24834, 23170, 21619, 20171, 18820, 17560]
+
+
+def _sm(x):
+    return int(splitmix64(np.uint64(x & M64)))
+
+
+def zipf_size(seed: int, d: int) -> int:
+    """Host restatement of zipf_doc_size (csrc/gen.hip)."""
+    h = _sm(seed ^ ((d << 24) | 0xF))
+    r, k = h % 733974, 0
+    while k < 19 and r >= ZIPF_W[k]:
+        r -= ZIPF_W[k]
+        k += 1
+    h2 = _sm(h)
+    span = 1 << k
+    a, b = (h2 & 0xFFFFF) % span, ((h2 >> 20) & 0xFFFFF) % span
+    return span + ((a * b) >> k)
+
+
+def zipf_docs(seed: int, docs):
+    """Host copy of the "zipf" workload (csrc/gen.hip) for doc ids `docs`."""
+    A, B = [], []
+    for d in docs:
+        size = zipf_size(seed, d)
+        g = [_sm(seed ^ ((d << 24) | (u << 4) | 1)) for u in range(size)]
+        a_del = [(x & 1) == 1 and (x & 2) == 0 for x in g]
+        b_del = [(x & 1) == 1 and (x & 2) != 0 for x in g]
+        na, nb = sum(b_del), sum(a_del)  # A re-adds where B deletes and vice versa
+        ea, eb, ra, rb = [], [], 0, 0
+        for u in range(size):
+            key = (d << 21) | u
+            if not a_del[u]:
+                if b_del[u]:
+                    ra += 1
+                    ea.append((key, 0, size + ra))
+                else:
+                    ea.append((key, 0, u + 1))
+            if not b_del[u]:
+                if a_del[u]:
+                    rb += 1
+                    eb.append((key, 1, rb))
+                else:
+                    eb.append((key, 0, u + 1))
+        A.append((ea, [size + na, 0]))
+        B.append((eb, [size, nb]))
+    return A, B
+
+
 def join_bytes(n_dst, n_src, n_out, R) -> int:
     """Σ over docs of 20(n_dst + n_src + n_out) + 24R + 12."""
     n_dst, n_src, n_out = (np.asarray(x, dtype=np.int64) for x in (n_dst, n_src, n_out))

@@ -37,6 +37,9 @@ hipError_t launch_gen_delta(uint64_t seed, uint32_t n_docs, uint32_t R, uint32_t
                             const SrcOutView& S, hipStream_t stream);
 hipError_t launch_gen_replicas(uint64_t seed, uint32_t n_docs, uint32_t P, uint32_t E, const OutView& D,
                                const SrcOutView& S, hipStream_t stream);
+hipError_t launch_gen_zipf(uint64_t seed, uint32_t n_docs, const uint32_t* offsets, const OutView& A,
+                           const OutView& B, hipStream_t stream);
+uint32_t host_zipf_doc_size(uint64_t seed, uint32_t d);
 }  // namespace crdt
 
 using namespace crdt;
@@ -331,6 +334,20 @@ int crdt_gen_replicas_async(crdt_ctx* ctx, uint64_t seed, uint32_t n_docs, uint3
                  (uint64_t*)w(srcs->counters), (uint32_t*)w(srcs->tomb_off), (uint64_t*)w(srcs->tkeys),
                  (uint32_t*)w(srcs->tactors), (uint64_t*)w(srcs->tcounters)};
     return hip_err(launch_gen_replicas(seed, n_docs, replicas, entries, view(dst), S, (hipStream_t)stream));
+}
+
+int crdt_gen_zipf_sizes(uint64_t seed, uint32_t n_docs, uint32_t* sizes) {
+    if (n_docs && !sizes) return CRDT_E_INVALID;
+    for (uint32_t d = 0; d < n_docs; ++d) sizes[d] = host_zipf_doc_size(seed, d);
+    return CRDT_OK;
+}
+
+int crdt_gen_zipf_async(crdt_ctx* ctx, uint64_t seed, uint32_t n_docs, const uint32_t* offsets,
+                        const crdt_awset_out* a, const crdt_awset_out* b, void* stream) {
+    if (!ctx || !offsets || !out_ptrs_ok(a) || !out_ptrs_ok(b) || n_docs >= (1u << 14)) return CRDT_E_INVALID;
+    int rc = set_device(ctx);
+    if (rc != CRDT_OK) return rc;
+    return hip_err(launch_gen_zipf(seed, n_docs, offsets, view(a), view(b), (hipStream_t)stream));
 }
 
 /* ---------------- validation (host) ---------------- */

@@ -291,6 +291,114 @@ hipError_t launch_gen_replicas(uint64_t seed, uint32_t n_docs, uint32_t P, uint3
     return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------
+// "zipf" workload (BASELINE config 4): skewed document sizes, 50% concurrent
+// add/remove conflicts, R = 2.
+//   size of doc d: octave k drawn with weight kZipfW[k] ~ 2^(-0.1k), k < 20
+//   (the Zipf(1.1) mass per octave), then 2^k + (a*b >> k) with a, b uniform
+//   in [0, 2^k) -- mean 3.4e4, max 2^20 - 1 (crdt_zipf_doc_size, host+device)
+//   base keys u < size (key = d << 21 | u): A added them in order (dots
+//   (A, u+1)), B merged A.  Then for each base key, G = splitmix64(seed ^
+//   (d << 24 | u << 4 | tag)): bit 0 of G(.,1) = conflict; bit 1 picks the
+//   side that deletes; the other side re-adds with a fresh dot (its re-adds in
+//   key order: A's counters continue from size, B's start at 1).
+__host__ __device__ inline uint64_t splitmix64_hd(uint64_t x) {
+    x += 0x9E3779B97F4A7C15ull;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+    return x ^ (x >> 31);
+}
+
+__host__ __device__ inline uint32_t zipf_doc_size(uint64_t seed, uint32_t d) {
+    const uint32_t W[20] = {65536, 61147, 57052, 53232, 49667, 46341, 43238, 40342, 37641, 35120,
+                            32768, 30574, 28526, 26616, 24834, 23170, 21619, 20171, 18820, 17560};
+    const uint64_t h = splitmix64_hd(seed ^ (((uint64_t)d << 24) | 0xFull));
+    uint32_t r = (uint32_t)(h % 733974u), k = 0;
+    while (k < 19 && r >= W[k]) r -= W[k++];
+    const uint64_t h2 = splitmix64_hd(h);
+    const uint64_t span = 1ull << k;
+    const uint64_t a = (h2 & 0xFFFFFull) % span, b = ((h2 >> 20) & 0xFFFFFull) % span;
+    return (uint32_t)(span + ((a * b) >> k));
+}
+
+__device__ __forceinline__ uint64_t zipf_G(uint64_t seed, uint32_t d, uint32_t u, uint32_t tag) {
+    return splitmix64(seed ^ (((uint64_t)d << 24) | ((uint64_t)u << 4) | tag));
+}
+
+// One wave per document, 64 base keys per iteration (ballot prefix carries).
+__global__ __launch_bounds__(256) void gen_zipf_kernel(uint64_t seed, uint32_t n_docs, const uint32_t* offsets,
+                                                        OutView A, OutView B) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t lt = low_mask(lane);
+    for (uint32_t d0 = blockIdx.x * 4 + (threadIdx.x >> 6); d0 < n_docs; d0 += gridDim.x * 4) {
+        const uint32_t d = uniform(d0);
+        const uint32_t size = zipf_doc_size(seed, d);
+        const uint32_t base = offsets[d];
+        uint32_t pa = 0, pb = 0, ra = 0, rb = 0;  // present so far (A, B); re-adds so far (A, B)
+        // pass 1: count re-adds of each side (VV and counters need the totals)
+        uint32_t na = 0, nb = 0;
+        for (uint32_t u0 = 0; u0 < size; u0 += 64) {
+            const uint32_t u = u0 + lane;
+            const uint64_t g = u < size ? zipf_G(seed, d, u, 1) : 0ull;
+            const bool conflict = u < size && (g & 1);
+            const bool a_del = conflict && !(g & 2);  // A deletes, B re-adds
+            na += popc(ballot(conflict && !a_del));
+            nb += popc(ballot(a_del));
+        }
+        for (uint32_t u0 = 0; u0 < size; u0 += 64) {
+            const uint32_t u = u0 + lane;
+            const bool in = u < size;
+            const uint64_t g = in ? zipf_G(seed, d, u, 1) : 0ull;
+            const bool conflict = in && (g & 1);
+            const bool a_del = conflict && !(g & 2);
+            const bool b_del = conflict && (g & 2);
+            const uint64_t key = ((uint64_t)d << 21) | u;
+            const uint64_t ma = ballot(in && !a_del), mb = ballot(in && !b_del);
+            const uint64_t mra = ballot(b_del), mrb = ballot(a_del);  // A re-adds where B deletes
+            if (in && !a_del) {
+                const uint32_t i = base + pa + popc(ma & lt);
+                A.keys[i] = key;
+                A.actors[i] = 0;
+                A.counters[i] = b_del ? (uint64_t)size + ra + popc(mra & lt) + 1 : (uint64_t)u + 1;
+            }
+            if (in && !b_del) {
+                const uint32_t i = base + pb + popc(mb & lt);
+                B.keys[i] = key;
+                B.actors[i] = a_del ? 1u : 0u;
+                B.counters[i] = a_del ? (uint64_t)rb + popc(mrb & lt) + 1 : (uint64_t)u + 1;
+            }
+            pa += popc(ma);
+            pb += popc(mb);
+            ra += popc(mra);
+            rb += popc(mrb);
+        }
+        if (lane == 0) {
+            A.offsets[d] = base;
+            B.offsets[d] = base;
+            A.counts[d] = pa;
+            B.counts[d] = pb;
+            if (d == n_docs - 1) {
+                A.offsets[n_docs] = base + size;
+                B.offsets[n_docs] = base + size;
+            }
+            A.vv[(size_t)d * 2] = (uint64_t)size + na;
+            A.vv[(size_t)d * 2 + 1] = 0;
+            B.vv[(size_t)d * 2] = size;
+            B.vv[(size_t)d * 2 + 1] = nb;
+        }
+    }
+}
+
+hipError_t launch_gen_zipf(uint64_t seed, uint32_t n_docs, const uint32_t* offsets, const OutView& A,
+                           const OutView& B, hipStream_t stream) {
+    if (n_docs == 0) return hipSuccess;
+    const uint32_t grid = (n_docs + 3) / 4;
+    hipLaunchKernelGGL(gen_zipf_kernel, dim3(grid), dim3(256), 0, stream, seed, n_docs, offsets, A, B);
+    return hipGetLastError();
+}
+
+uint32_t host_zipf_doc_size(uint64_t seed, uint32_t d) { return zipf_doc_size(seed, d); }
+
 hipError_t launch_gen_pair(uint64_t seed, uint32_t n_docs, const OutView& A, const OutView& B, hipStream_t stream) {
     if (n_docs == 0) return hipSuccess;
     uint32_t grid = (n_docs + 3) / 4;

@@ -410,3 +410,40 @@ def test_gen_replicas_and_config5_fold(eng, torch):
     ho = host_out(out, torch)
     assert_same_all(ho, want, n, R)
     assert ctx.cpu().numpy().view(np.uint64).tolist() == oracle.causal_context(want.vv, n, R).tolist()
+
+
+def gen_zipf(eng, torch, n, seed=0x5EED):
+    from crdtgpu.engine import zipf_sizes
+
+    dev = torch.device("cuda:0")
+    sizes = zipf_sizes(seed, n)
+    offs = np.zeros(n + 1, dtype=np.uint32)
+    np.cumsum(sizes, out=offs[1:])
+    total = int(offs[-1])
+    d_offs = torch.from_numpy(offs.view(np.int32).copy()).to(dev)
+    A = OutBuffers(n, 2, total, device=dev)
+    B = OutBuffers(n, 2, total, device=dev)
+    eng.gen_zipf_async(seed, n, d_offs, A, B)
+    eng.sync()
+    return A, B, total
+
+
+def test_config4_zipf_slice_exact(eng, torch):
+    """Config 4 (Zipf sizes up to 2^20, 50% add/remove conflicts) on the first
+    1,024 docs: generator vs host restatement on small docs; both join
+    directions exact on every doc (wave + block paths) vs the oracle."""
+    n = 1024
+    A, B, total = gen_zipf(eng, torch, n)
+    ha, hb = host_out(A, torch), host_out(B, torch)
+    small = [d for d in range(64) if workloads.zipf_size(0x5EED, d) <= 3000][:12]
+    wa, wb = workloads.zipf_docs(0x5EED, small)
+    for i, d in enumerate(small):
+        assert out_doc(ha, d, 2) == wa[i] and out_doc(hb, d, 2) == wb[i]
+    dev = torch.device("cuda:0")
+    for x, y, hx, hy in ((A, B, ha, hb), (B, A, hb, ha)):
+        o = OutBuffers(n, 2, 2 * total, device=dev)
+        eng.join_async(x.as_batch(), y.as_batch(), o)
+        eng.sync()
+        rc, want = oracle.join(hx.as_batch(), hy.as_batch())
+        assert rc == 0
+        assert_same_all(host_out(o, torch), want, n, 2)

@@ -87,3 +87,33 @@ def test_replica_workload_is_consistent():
         for r, v, e, t in states:
             assert len(e) == 16 and not t and v[r] >= 16
             assert all(v[a] >= c >= 1 for _, a, c in e)
+
+
+def replay_zipf(seed, d):
+    """The op history that defines doc d of the zipf workload (config 4)."""
+    size = workloads.zipf_size(seed, d)
+    key = lambda u: (d << 21) | u  # noqa: E731
+    A = ref.AWSet(0, ref.VersionVector([0, 0]))
+    B = ref.AWSet(1, ref.VersionVector([0, 0]))
+    A.Add(*[key(u) for u in range(size)])
+    B.Merge(A)
+    g = [workloads._sm(seed ^ ((d << 24) | (u << 4) | 1)) for u in range(size)]
+    a_del = [u for u in range(size) if g[u] & 1 and not g[u] & 2]
+    b_del = [u for u in range(size) if g[u] & 1 and g[u] & 2]
+    A.Del(*[key(u) for u in a_del])
+    B.Del(*[key(u) for u in b_del])
+    A.Add(*[key(u) for u in b_del])  # concurrent re-add wins over the other side's delete
+    B.Add(*[key(u) for u in a_del])
+    return A, B
+
+
+def test_zipf_workload_is_reachable_and_skewed():
+    docs = [d for d in range(64) if workloads.zipf_size(0x5EED, d) <= 5000][:25]
+    A, B = workloads.zipf_docs(0x5EED, docs)
+    for i, d in enumerate(docs):
+        a, b = replay_zipf(0x5EED, d)
+        assert A[i] == as_doc(a) and B[i] == as_doc(b)
+    sizes = [workloads.zipf_size(0x5EED, d) for d in range(4096)]
+    assert 1 <= min(sizes) and max(sizes) < (1 << 20)
+    assert 20_000 < sum(sizes) / len(sizes) < 50_000
+    assert sorted(sizes)[len(sizes) // 2] < 5000  # heavy tail: median far below the mean

@@ -4,7 +4,7 @@ set -u
 cd "$(dirname "$0")/.."
 mkdir -p gpurun_out
 TAG=${TAG:-r01}
-for c in ${CONFIGS:-3 5}; do
+for c in ${CONFIGS:-3 4 5}; do
   timeout -k 10 300 python bench.py --config $c > gpurun_out/bench_c$c.log 2>&1
   rc=$?; echo "[bench config $c] rc=$rc"; tail -2 gpurun_out/bench_c$c.log | cut -c1-2000
   if [ $rc -ne 0 ]; then exit $rc; fi
