@@ -344,7 +344,7 @@ int crdt_gen_zipf_sizes(uint64_t seed, uint32_t n_docs, uint32_t* sizes) {
 
 int crdt_gen_zipf_async(crdt_ctx* ctx, uint64_t seed, uint32_t n_docs, const uint32_t* offsets,
                         const crdt_awset_out* a, const crdt_awset_out* b, void* stream) {
-    if (!ctx || !offsets || !out_ptrs_ok(a) || !out_ptrs_ok(b) || n_docs >= (1u << 14)) return CRDT_E_INVALID;
+    if (!ctx || !offsets || !out_ptrs_ok(a) || !out_ptrs_ok(b) || n_docs >= (1u << 24)) return CRDT_E_INVALID;
     int rc = set_device(ctx);
     if (rc != CRDT_OK) return rc;
     return hip_err(launch_gen_zipf(seed, n_docs, offsets, view(a), view(b), (hipStream_t)stream));

@@ -168,7 +168,7 @@ int crdt_gen_delta_async(crdt_ctx* ctx, uint64_t seed, uint32_t n_docs, uint32_t
  * entries (a power of two <= 32), R = replicas; dst = replica 0 (entries slots
  * per doc), srcs = replicas 1.. in order (entries slots each, 0 tombstones;
  * tomb_off must be allocated).  Fold with CRDT_FOLD_AWSET. */
-/* "zipf" (BASELINE config 4): n_docs (< 16384) docs, sizes from
+/* "zipf" (BASELINE config 4): n_docs (< 2^24) docs, sizes from
  * crdt_gen_zipf_sizes (host, no GPU), A/B replicas with 50% concurrent
  * add/remove conflicts, R = 2.  offsets: device array [n_docs+1], the prefix
  * sum of the sizes (each side gets `size` slots per doc).  Formulas: gen.hip. */
