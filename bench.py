@@ -69,6 +69,8 @@ class Config2:
     kernel = "join_wave_kernel"
     metric = "replica-merges/sec (AWSet full-state join) + achieved HBM GB/s (% roofline)"
 
+    exchange = True  # both directions from one read (crdt_awset_exchange_async); --separate: two joins
+
     def __init__(self, eng, n, seed, dev, stream):
         import torch
 
@@ -90,14 +92,18 @@ class Config2:
         self.n_events = 3
 
     def step(self, ev=None):
-        """Both joins; returns the local causal-context summary tensor."""
+        """A <- B and B <- A for every doc; returns the local causal-context summary."""
         s, eng, n, R = self.stream, self.eng, self.n, self.R
         if ev is not None:
             ev[0].record(s)
-        eng.join_async(self.a, self.b, self.oab, stream=s)
+        if self.exchange:
+            eng.exchange_async(self.a, self.b, self.oab, self.oba, stream=s)
+        else:
+            eng.join_async(self.a, self.b, self.oab, stream=s)
         if ev is not None:
             ev[1].record(s)
-        eng.join_async(self.b, self.a, self.oba, stream=s)
+        if not self.exchange:
+            eng.join_async(self.b, self.a, self.oba, stream=s)
         if ev is not None:
             ev[2].record(s)
         eng.causal_context_async(self.oab.vv, n, R, self.ctx_ab, stream=s)
@@ -106,21 +112,30 @@ class Config2:
         return self.ctx_ab
 
     def launch_seconds(self, events, steps):
+        """Mean duration of one launch of the dominant kernel (exchange: the one launch)."""
         t_ab = sum(e[0].elapsed_time(e[1]) for e in events) / steps / 1e3
+        if self.exchange:
+            return t_ab
         t_ba = sum(e[1].elapsed_time(e[2]) for e in events) / steps / 1e3
         return (t_ab + t_ba) / 2
 
     def bytes_per_launch(self):
+        """SURVEY 8d per-merge bytes x the merges one launch performs (exchange: 2 per doc)."""
         from crdtgpu import workloads
 
         cA, cB = self.A.counts.cpu().numpy(), self.B.counts.cpu().numpy()
         b1 = workloads.join_bytes(cA, cB, self.oab.counts.cpu().numpy(), self.R)
         b2 = workloads.join_bytes(cB, cA, self.oba.counts.cpu().numpy(), self.R)
-        return (b1 + b2) // 2
+        return (b1 + b2) if self.exchange else (b1 + b2) // 2
+
+    @property
+    def kernel_name(self):
+        return self.kernel + (" (exchange: both directions, one read)" if self.exchange else "")
 
     def describe(self, world):
         return {"workload": "config2: %d docs/GPU x 2 replicas x 64 entries, R=2, full-state join both directions "
-                            "+ causal-context allreduce(max,u64)" % self.n,
+                            "(%s) + causal-context allreduce(max,u64)" % (
+                                self.n, "one exchange launch" if self.exchange else "two join launches"),
                 "docs_per_gpu": self.n, "replicas": 2, "entries_per_replica": 64, "R": self.R,
                 "merges_per_step": self.merges_per_step * world, "parallelism": "doc-sharded x%d" % world}
 
@@ -378,6 +393,7 @@ def main():
     ap.add_argument("--cpu-sample", type=int, default=65536)
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--separate", action="store_true", help="configs 2/4: two join launches instead of one exchange")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"))
     args = ap.parse_args()
 
@@ -404,7 +420,10 @@ def main():
     eng = crdtgpu.Engine(local)
     # each rank owns its own documents (weak scaling; no data-path exchange)
     seed = args.seed + (rank << 40)
-    W = {2: Config2, 3: Config3, 4: Config4, 5: Config5}[args.config](eng, n, seed, dev, stream)
+    cls = {2: Config2, 3: Config3, 4: Config4, 5: Config5}[args.config]
+    if args.separate:
+        cls.exchange = False
+    W = cls(eng, n, seed, dev, stream)
     eng.sync(stream)
 
     def step(ev=None):
@@ -444,7 +463,9 @@ def main():
     if os.path.exists(args.traffic_json):
         try:
             tj = json.load(open(args.traffic_json))
-            if tj.get("docs") == n and tj.get("kernel", "").startswith(W.kernel):
+            if (tj.get("docs") == n and tj.get("kernel", "").startswith(W.kernel)
+                    and bool(tj.get("exchange", False)) == bool(getattr(W, "exchange", False))
+                    and tj.get("config", 2) == args.config):
                 traffic = tj.get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
@@ -466,11 +487,14 @@ def main():
         "config": W.describe(world),
         "roofline": {
             "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": W.kernel,
+            "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": getattr(W, "kernel_name", W.kernel),
             "algorithmic_bytes_per_launch": bytes_launch, "launch_ms": t_launch * 1e3,
         },
         "global_causal_context": global_ctx,
     }
+    if traffic:
+        result["roofline"]["traffic_gbs"] = traffic / t_launch / 1e9
+        result["roofline"]["traffic_frac"] = traffic / t_launch / 1e9 / HBM_PEAK_GBS
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = W.cpu_baseline(min(args.cpu_sample, n), args.cpu_budget)
     if rank == 0:

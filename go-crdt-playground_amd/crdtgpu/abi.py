@@ -107,6 +107,9 @@ def _load():
         "crdt_ctx_set_max_doc_entries": (ctypes.c_int, [_vp, _u32]),
         "crdt_ctx_set_option": (ctypes.c_int, [_vp, ctypes.c_char_p, ctypes.c_int64]),
         "crdt_awset_join_async": (ctypes.c_int, [_vp, P(CAWSetBatch), P(CAWSetBatch), P(CAWSetOut), _vp]),
+        "crdt_awset_exchange_async": (ctypes.c_int, [_vp, P(CAWSetBatch), P(CAWSetBatch), P(CAWSetOut),
+                                                     P(CAWSetOut), _vp]),
+        "crdt_awset_exchange_batch": (ctypes.c_int, [_vp, P(CAWSetBatch), P(CAWSetBatch), P(CAWSetOut), P(CAWSetOut)]),
         "crdt_awset_fold_async": (ctypes.c_int, [_vp, ctypes.c_int, P(CAWSetBatch), P(CSrcBatch), P(CAWSetOut), _vp]),
         "crdt_vv_max_async": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_size_t, _vp]),
         "crdt_causal_context_async": (ctypes.c_int, [_vp, _vp, _u32, _u32, _vp, _vp]),

@@ -61,6 +61,11 @@ class Engine:
         check(self._lib.crdt_awset_join_async(self._ctx, ctypes.byref(d), ctypes.byref(s), ctypes.byref(o),
                                               _stream(stream)), "crdt_awset_join_async")
 
+    def exchange_async(self, a: AWSetBatch, b: AWSetBatch, out_ab: OutBuffers, out_ba: OutBuffers, stream=None):
+        ca, cb, o1, o2 = a.c(), b.c(), out_ab.c(), out_ba.c()
+        check(self._lib.crdt_awset_exchange_async(self._ctx, ctypes.byref(ca), ctypes.byref(cb), ctypes.byref(o1),
+                                                  ctypes.byref(o2), _stream(stream)), "crdt_awset_exchange_async")
+
     def fold_async(self, mode: int, dst: AWSetBatch, srcs: SrcBatch, out: OutBuffers, stream=None):
         d, s, o = dst.c(), srcs.c(), out.c()
         check(self._lib.crdt_awset_fold_async(self._ctx, int(mode), ctypes.byref(d), ctypes.byref(s),
@@ -103,6 +108,15 @@ class Engine:
         check(self._lib.crdt_awset_join_batch(self._ctx, ctypes.byref(d), ctypes.byref(s), ctypes.byref(o)),
               "crdt_awset_join_batch")
         return out
+
+    def exchange(self, a: AWSetBatch, b: AWSetBatch):
+        a, b = a.numpy(), b.numpy()
+        slots = int(a.offsets[-1]) + int(b.offsets[-1])
+        o1, o2 = OutBuffers(a.n_docs, a.R, slots), OutBuffers(a.n_docs, a.R, slots)
+        ca, cb, c1, c2 = a.c(), b.c(), o1.c(), o2.c()
+        check(self._lib.crdt_awset_exchange_batch(self._ctx, ctypes.byref(ca), ctypes.byref(cb), ctypes.byref(c1),
+                                                  ctypes.byref(c2)), "crdt_awset_exchange_batch")
+        return o1, o2
 
     def fold(self, mode: int, dst: AWSetBatch, srcs: SrcBatch) -> OutBuffers:
         dst, srcs = dst.numpy(), srcs.numpy()

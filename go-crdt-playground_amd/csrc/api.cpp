@@ -11,8 +11,8 @@
 #include "crdt_device.hpp"
 
 namespace crdt {
-hipError_t launch_join(const BatchView& dst, const BatchView& src, const OutView& out, const Work& wk,
-                       uint32_t docs_per_wave, bool nt_stores, uint32_t block_grid, bool no_large,
+hipError_t launch_join(const BatchView& dst, const BatchView& src, const OutView& out, const OutView* out2,
+                       const Work& wk, uint32_t docs_per_wave, bool nt_stores, uint32_t block_grid, bool no_large,
                        hipStream_t stream);
 hipError_t launch_fold(int mode, const BatchView& dst, const SrcView& sb, const OutView& out, const Scratch& scr,
                        const Work& wk, uint32_t block_grid, hipStream_t stream);
@@ -88,7 +88,7 @@ struct crdt_ctx {
     uint32_t join_docs_per_wave = 8;          // crdt_ctx_set_option("join_docs_per_wave")
     bool join_nt_stores = true;               // crdt_ctx_set_option("join_nt_stores")
     // staging for the *_batch host path
-    DevBuf stage[24];
+    DevBuf stage[32];
     hipStream_t stream = nullptr;
 };
 
@@ -247,18 +247,33 @@ int crdt_ctx_sync(crdt_ctx* ctx, void* stream) {
     return CRDT_OK;
 }
 
-int crdt_awset_join_async(crdt_ctx* ctx, const crdt_awset_batch* dst, const crdt_awset_batch* src,
-                          const crdt_awset_out* out, void* stream) {
-    if (!ctx || !batch_ptrs_ok(dst) || !batch_ptrs_ok(src) || !out_ptrs_ok(out)) return CRDT_E_INVALID;
+static int join_common(crdt_ctx* ctx, const crdt_awset_batch* dst, const crdt_awset_batch* src,
+                       const crdt_awset_out* out, const crdt_awset_out* out2, void* stream) {
+    if (!ctx || !batch_ptrs_ok(dst) || !batch_ptrs_ok(src) || !out_ptrs_ok(out) || (out2 && !out_ptrs_ok(out2)))
+        return CRDT_E_INVALID;
     if (dst->n_docs != src->n_docs || dst->R != src->R) return CRDT_E_INVALID;
     int rc = set_device(ctx);
     if (rc == CRDT_OK) rc = reserve_worklist(ctx, dst->n_docs);
     if (rc != CRDT_OK) return rc;
     hipStream_t s = (hipStream_t)stream;
-    if (hipMemsetAsync(ctx->ws.p, 0, 64, s) != hipSuccess) return CRDT_E_HIP;
-    return hip_err(launch_join(view(dst), view(src), view(out), make_work(ctx), ctx->join_docs_per_wave, ctx->join_nt_stores,
-                               block_grid(ctx),
-                               ctx->max_doc_entries <= 64, s));
+    const bool no_large = ctx->max_doc_entries <= 64;
+    // the per-call counters are read only by the block path
+    if (!no_large && hipMemsetAsync(ctx->ws.p, 0, 64, s) != hipSuccess) return CRDT_E_HIP;
+    OutView o2v;
+    if (out2) o2v = view(out2);
+    return hip_err(launch_join(view(dst), view(src), view(out), out2 ? &o2v : nullptr, make_work(ctx),
+                               ctx->join_docs_per_wave, ctx->join_nt_stores, block_grid(ctx), no_large, s));
+}
+
+int crdt_awset_join_async(crdt_ctx* ctx, const crdt_awset_batch* dst, const crdt_awset_batch* src,
+                          const crdt_awset_out* out, void* stream) {
+    return join_common(ctx, dst, src, out, nullptr, stream);
+}
+
+int crdt_awset_exchange_async(crdt_ctx* ctx, const crdt_awset_batch* a, const crdt_awset_batch* b,
+                              const crdt_awset_out* out_ab, const crdt_awset_out* out_ba, void* stream) {
+    if (!out_ab || !out_ba || out_ab->keys == out_ba->keys) return CRDT_E_INVALID;
+    return join_common(ctx, a, b, out_ab, out_ba, stream);
 }
 
 int crdt_awset_fold_async(crdt_ctx* ctx, int mode, const crdt_awset_batch* dst, const crdt_src_batch* srcs,
@@ -474,6 +489,28 @@ int crdt_awset_join_batch(crdt_ctx* ctx, const crdt_awset_batch* dst, const crdt
     if (st.rc != CRDT_OK) return st.rc;
     rc = crdt_awset_join_async(ctx, &dd, &ds, &dout, ctx->stream);
     if (rc == CRDT_OK) rc = fetch_out(out, dout, dst->n_docs, dst->R, slots, ctx->stream);
+    const int sync = crdt_ctx_sync(ctx, ctx->stream);
+    return rc != CRDT_OK ? rc : sync;
+}
+
+int crdt_awset_exchange_batch(crdt_ctx* ctx, const crdt_awset_batch* a, const crdt_awset_batch* b,
+                              const crdt_awset_out* out_ab, const crdt_awset_out* out_ba) {
+    if (!ctx || !out_ptrs_ok(out_ab) || !out_ptrs_ok(out_ba)) return CRDT_E_INVALID;
+    int rc = crdt_validate_batch(a);
+    if (rc == CRDT_OK) rc = crdt_validate_batch(b);
+    if (rc != CRDT_OK) return rc;
+    if (a->n_docs != b->n_docs || a->R != b->R) return CRDT_E_INVALID;
+    if ((uint64_t)a->offsets[a->n_docs] + b->offsets[b->n_docs] >= (1ull << 32)) return CRDT_E_INVALID;
+    if ((rc = set_device(ctx)) != CRDT_OK) return rc;
+    Stager st{ctx};
+    crdt_awset_batch da = stage_batch(st, a), db = stage_batch(st, b);
+    const size_t slots = (size_t)a->offsets[a->n_docs] + b->offsets[b->n_docs];
+    crdt_awset_out o1 = stage_out(st, a->n_docs, a->R, slots);
+    crdt_awset_out o2 = stage_out(st, a->n_docs, a->R, slots);
+    if (st.rc != CRDT_OK) return st.rc;
+    rc = crdt_awset_exchange_async(ctx, &da, &db, &o1, &o2, ctx->stream);
+    if (rc == CRDT_OK) rc = fetch_out(out_ab, o1, a->n_docs, a->R, slots, ctx->stream);
+    if (rc == CRDT_OK) rc = fetch_out(out_ba, o2, a->n_docs, a->R, slots, ctx->stream);
     const int sync = crdt_ctx_sync(ctx, ctx->stream);
     return rc != CRDT_OK ? rc : sync;
 }

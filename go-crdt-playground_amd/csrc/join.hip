@@ -84,10 +84,16 @@ struct JoinWaveSmem {
 
 // Merge document d whose entries are in L (awset.go:107-161).  AUX: cache
 // policy of the entry stores (0 plain, kAuxNT non-temporal).
-template <int WAVES, int AUX>
+// EXCH: also write out2 = src <- dst (the exchange's other direction).  Both
+// directions keep the same keys at the same slots (a dst-only key survives iff
+// srcVV has not seen it, a src-only key iff dstVV has not, in either
+// direction); only a common key's dot differs -- the src dot wins
+// (awset.go:142), so out2 takes the dst lane's own dot.
+template <int WAVES, int AUX, bool EXCH>
 __device__ __forceinline__ void join_doc(JoinWaveSmem<WAVES>& sm, uint32_t w, const JoinLanes& L, const JoinMeta& m,
-                                         uint32_t d, bool small, const OutView& out, uint32_t n_docs,
-                                         uint32_t end_off, uint32_t R, uint32_t lane, uint64_t lt, uint32_t& err) {
+                                         uint32_t d, bool small, const OutView& out, const OutView& out2,
+                                         uint32_t n_docs, uint32_t end_off, uint32_t R, uint32_t lane, uint64_t lt,
+                                         uint32_t& err) {
     const uint32_t obase = m.doff + m.soff;
     const uint32_t dnn = small ? m.dn : 0u, snn = small ? m.sn : 0u;
     const bool dv = lane < dnn, sv = lane < snn;
@@ -127,10 +133,24 @@ __device__ __forceinline__ void join_doc(JoinWaveSmem<WAVES>& sm, uint32_t w, co
     st64<AUX>(L.sc, oc, s8);
     // slot bounds (every doc), live count and VV (wave path only)
     const bool last = d == n_docs - 1;
+    const uint64_t vmax = L.vd > L.vs ? L.vd : L.vs;  // awset.go:160 -> crdt-misc.go:43-55
     st32(lane == 0 ? obase : end_off, make_rsrc(out.offsets + d, last ? 8u : 4u), lane < 2 ? lane * 4u : kOOB);
     st32(popc(dm) + popc(smk), make_rsrc(out.counts + d, small ? 4u : 0u), lane == 0 ? 0u : kOOB);
-    // awset.go:160 -> crdt-misc.go:43-55
-    st64(L.vd > L.vs ? L.vd : L.vs, make_rsrc(out.vv + (size_t)d * R, small ? R * 8u : 0u), lane * 8u);
+    st64(vmax, make_rsrc(out.vv + (size_t)d * R, small ? R * 8u : 0u), lane * 8u);
+    if (EXCH) {
+        const rsrc_t pk = make_rsrc(out2.keys + obase, cap * 8u);
+        const rsrc_t pa = make_rsrc(out2.actors + obase, cap * 4u);
+        const rsrc_t pc = make_rsrc(out2.counters + obase, cap * 8u);
+        st64<AUX>(L.dk, pk, d8);
+        st32<AUX>(L.da, pa, d4);
+        st64<AUX>(L.dc, pc, d8);
+        st64<AUX>(L.sk, pk, s8);
+        st32<AUX>(L.sa, pa, s4);
+        st64<AUX>(L.sc, pc, s8);
+        st32(lane == 0 ? obase : end_off, make_rsrc(out2.offsets + d, last ? 8u : 4u), lane < 2 ? lane * 4u : kOOB);
+        st32(popc(dm) + popc(smk), make_rsrc(out2.counts + d, small ? 4u : 0u), lane == 0 ? 0u : kOOB);
+        st64(vmax, make_rsrc(out2.vv + (size_t)d * R, small ? R * 8u : 0u), lane * 8u);
+    }
     wave_sync();
 }
 
@@ -141,9 +161,9 @@ __device__ __forceinline__ void join_doc(JoinWaveSmem<WAVES>& sm, uint32_t w, co
 // ping-pong pipeline -- the next document's entries are issued before this
 // one is merged.  The body is straight-line buffer VMEM, so the compiler's
 // vmcnt waits count exactly and the prefetch stays in flight.
-template <int WAVES, int K, int AUX>
-__global__ __launch_bounds__(WAVES * 64) void join_wave_kernel(BatchView dst, BatchView src, OutView out, Work wk,
-                                                               uint32_t no_large) {
+template <int WAVES, int K, int AUX, bool EXCH>
+__global__ __launch_bounds__(WAVES * 64) void join_wave_kernel(BatchView dst, BatchView src, OutView out, OutView out2,
+                                                               Work wk, uint32_t no_large) {
     __shared__ JoinWaveSmem<WAVES> sm;
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t w = threadIdx.x >> 6;
@@ -180,7 +200,7 @@ __global__ __launch_bounds__(WAVES * 64) void join_wave_kernel(BatchView dst, Ba
         uint32_t dn = d + WAVES;
         bool small_n = more && mn.dn <= 64 && mn.sn <= 64;
         lanes_issue(LB, dst, src, mn, dn, small_n, lane, R);
-        join_doc<WAVES, AUX>(sm, w, LA, m, d, small, out, n_docs, end_off, R, lane, lt, err);
+        join_doc<WAVES, AUX, EXCH>(sm, w, LA, m, d, small, out, out2, n_docs, end_off, R, lane, lt, err);
         if (!small) push_large(d);
         if (!more) break;
         ++k;
@@ -193,7 +213,7 @@ __global__ __launch_bounds__(WAVES * 64) void join_wave_kernel(BatchView dst, Ba
         dn = d + WAVES;
         small_n = more && mn.dn <= 64 && mn.sn <= 64;
         lanes_issue(LA, dst, src, mn, dn, small_n, lane, R);
-        join_doc<WAVES, AUX>(sm, w, LB, m, d, small, out, n_docs, end_off, R, lane, lt, err);
+        join_doc<WAVES, AUX, EXCH>(sm, w, LB, m, d, small, out, out2, n_docs, end_off, R, lane, lt, err);
         if (!small) push_large(d);
         if (!more) break;
         ++k;
@@ -204,15 +224,18 @@ __global__ __launch_bounds__(WAVES * 64) void join_wave_kernel(BatchView dst, Ba
     flag_error(wk.status, err);
 }
 
+// head: which dequeue counter this pass uses (the exchange runs the worklist
+// twice, once per direction).
 template <int NT, int IPT>
-__global__ __launch_bounds__(NT) void join_block_kernel(BatchView dst, BatchView src, OutView out, Work wk) {
+__global__ __launch_bounds__(NT) void join_block_kernel(BatchView dst, BatchView src, OutView out, Work wk,
+                                                        uint32_t head) {
     __shared__ MergeSmem<NT, IPT> sm;
     const uint32_t tid = threadIdx.x;
     const uint32_t R = dst.R;
     uint32_t err = 0;
     const Entries none{nullptr, nullptr, nullptr, 0};
     for (;;) {
-        if (tid == 0) sm.word[0] = atomicAdd(wk.wl_head, 1u);
+        if (tid == 0) sm.word[0] = atomicAdd(wk.wl_head + head, 1u);
         __syncthreads();
         const uint32_t slot = sm.word[0];
         const uint32_t total = __hip_atomic_load(wk.wl_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -241,43 +264,57 @@ constexpr int kJoinWaves = 4;
 constexpr int kBlockNT = 256;
 constexpr int kBlockIPT = 4;
 
-template <int K, int AUX>
-static void launch_wave(const BatchView& dst, const BatchView& src, const OutView& out, const Work& wk, bool no_large,
-                        hipStream_t stream) {
+template <int K, int AUX, bool EXCH>
+static void launch_wave(const BatchView& dst, const BatchView& src, const OutView& out, const OutView& out2,
+                        const Work& wk, bool no_large, hipStream_t stream) {
     const uint32_t per_block = kJoinWaves * K;
     const uint32_t grid = (dst.n_docs + per_block - 1) / per_block;
-    hipLaunchKernelGGL((join_wave_kernel<kJoinWaves, K, AUX>), dim3(grid), dim3(kJoinWaves * 64), 0, stream, dst, src,
-                       out, wk, (uint32_t)no_large);
+    hipLaunchKernelGGL((join_wave_kernel<kJoinWaves, K, AUX, EXCH>), dim3(grid), dim3(kJoinWaves * 64), 0, stream,
+                       dst, src, out, out2, wk, (uint32_t)no_large);
 }
 
-template <int AUX>
-static void launch_wave_k(uint32_t k, const BatchView& dst, const BatchView& src, const OutView& out, const Work& wk,
-                          bool no_large, hipStream_t stream) {
+template <int AUX, bool EXCH>
+static void launch_wave_k(uint32_t k, const BatchView& dst, const BatchView& src, const OutView& out,
+                          const OutView& out2, const Work& wk, bool no_large, hipStream_t stream) {
     switch (k) {
-        case 1: launch_wave<1, AUX>(dst, src, out, wk, no_large, stream); break;
-        case 2: launch_wave<2, AUX>(dst, src, out, wk, no_large, stream); break;
-        case 4: launch_wave<4, AUX>(dst, src, out, wk, no_large, stream); break;
-        case 16: launch_wave<16, AUX>(dst, src, out, wk, no_large, stream); break;
-        default: launch_wave<8, AUX>(dst, src, out, wk, no_large, stream); break;
+        case 1: launch_wave<1, AUX, EXCH>(dst, src, out, out2, wk, no_large, stream); break;
+        case 2: launch_wave<2, AUX, EXCH>(dst, src, out, out2, wk, no_large, stream); break;
+        case 4: launch_wave<4, AUX, EXCH>(dst, src, out, out2, wk, no_large, stream); break;
+        case 16: launch_wave<16, AUX, EXCH>(dst, src, out, out2, wk, no_large, stream); break;
+        default: launch_wave<8, AUX, EXCH>(dst, src, out, out2, wk, no_large, stream); break;
     }
 }
 
 // docs_per_wave: K of join_wave_kernel (1, 2, 4, 8 or 16); nt_stores: write the
 // output with non-temporal stores; no_large: the caller promised every doc has
 // <= 64 entries per side, so the block path is not launched (a larger doc then
-// raises CRDT_E_INVALID).
-hipError_t launch_join(const BatchView& dst, const BatchView& src, const OutView& out, const Work& wk,
-                       uint32_t docs_per_wave, bool nt_stores, uint32_t block_grid, bool no_large,
+// raises CRDT_E_INVALID).  out2 != nullptr: exchange -- also out2 = src <- dst.
+hipError_t launch_join(const BatchView& dst, const BatchView& src, const OutView& out, const OutView* out2,
+                       const Work& wk, uint32_t docs_per_wave, bool nt_stores, uint32_t block_grid, bool no_large,
                        hipStream_t stream) {
     if (dst.n_docs == 0) return hipSuccess;
-    if (nt_stores)
-        launch_wave_k<kAuxNT>(docs_per_wave, dst, src, out, wk, no_large, stream);
-    else
-        launch_wave_k<0>(docs_per_wave, dst, src, out, wk, no_large, stream);
+    const OutView& o2 = out2 ? *out2 : out;
+    if (out2) {
+        if (nt_stores)
+            launch_wave_k<kAuxNT, true>(docs_per_wave, dst, src, out, o2, wk, no_large, stream);
+        else
+            launch_wave_k<0, true>(docs_per_wave, dst, src, out, o2, wk, no_large, stream);
+    } else {
+        if (nt_stores)
+            launch_wave_k<kAuxNT, false>(docs_per_wave, dst, src, out, o2, wk, no_large, stream);
+        else
+            launch_wave_k<0, false>(docs_per_wave, dst, src, out, o2, wk, no_large, stream);
+    }
     hipError_t e = hipGetLastError();
     if (e != hipSuccess || no_large) return e;
     hipLaunchKernelGGL((join_block_kernel<kBlockNT, kBlockIPT>), dim3(block_grid), dim3(kBlockNT), 0, stream, dst,
-                       src, out, wk);
+                       src, out, wk, 0u);
+    if (out2) {
+        e = hipGetLastError();
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL((join_block_kernel<kBlockNT, kBlockIPT>), dim3(block_grid), dim3(kBlockNT), 0, stream,
+                           src, dst, *out2, wk, 1u);
+    }
     return hipGetLastError();
 }
 

@@ -144,6 +144,12 @@ int crdt_abi_version(void);
 /* ---- device-resident, asynchronous on a HIP stream (NULL = default) ---- */
 int crdt_awset_join_async(crdt_ctx* ctx, const crdt_awset_batch* dst, const crdt_awset_batch* src,
                           const crdt_awset_out* out, void* stream);
+/* Anti-entropy exchange: out_ab[d] = a[d] <- b[d] AND out_ba[d] = b[d] <- a[d]
+ * (two (*AWSet).Merge calls per doc, awset.go:103-161) from ONE read of both
+ * states.  Both directions keep the same keys at the same slots; only a
+ * common key's dot differs (the src dot wins, awset.go:142). */
+int crdt_awset_exchange_async(crdt_ctx* ctx, const crdt_awset_batch* a, const crdt_awset_batch* b,
+                              const crdt_awset_out* out_ab, const crdt_awset_out* out_ba, void* stream);
 int crdt_awset_fold_async(crdt_ctx* ctx, int mode, const crdt_awset_batch* dst, const crdt_src_batch* srcs,
                           const crdt_awset_out* out, void* stream);
 /* dst[i] = max(dst[i], src[i]) for i < n (u64). */
@@ -181,6 +187,8 @@ int crdt_gen_replicas_async(crdt_ctx* ctx, uint64_t seed, uint32_t n_docs, uint3
 /* ---- host buffers, synchronous: copies in, runs, copies out ------------- */
 int crdt_awset_join_batch(crdt_ctx* ctx, const crdt_awset_batch* dst, const crdt_awset_batch* src,
                           const crdt_awset_out* out);
+int crdt_awset_exchange_batch(crdt_ctx* ctx, const crdt_awset_batch* a, const crdt_awset_batch* b,
+                              const crdt_awset_out* out_ab, const crdt_awset_out* out_ba);
 int crdt_awset_fold_batch(crdt_ctx* ctx, int mode, const crdt_awset_batch* dst, const crdt_src_batch* srcs,
                           const crdt_awset_out* out);
 

@@ -447,3 +447,56 @@ def test_config4_zipf_slice_exact(eng, torch):
         rc, want = oracle.join(hx.as_batch(), hy.as_batch())
         assert rc == 0
         assert_same_all(host_out(o, torch), want, n, 2)
+
+
+@pytest.mark.parametrize("sizes", ["small", "mixed"])
+def test_exchange_equals_two_joins(eng, torch, sizes):
+    """crdt_awset_exchange_*: one pass, out_ab = a <- b and out_ba = b <- a,
+    each bit-exact vs the oracle join (wave path, and block path for > 64)."""
+    rng = random.Random(40 if sizes == "small" else 41)
+    R = 3
+    pick = (lambda: rng.randint(0, 64)) if sizes == "small" else (lambda: rng.choice([0, 5, 64, 65, 300, 2000]))
+    a, b = join_case(rng, 1500 if sizes == "small" else 300, R, pick, 5000, 9)
+    o1, o2 = eng.exchange(a, b)
+    rc, w1 = oracle.join(a, b)
+    assert rc == 0
+    rc, w2 = oracle.join(b, a)
+    assert rc == 0
+    assert_same(o1, w1, a.n_docs, R)
+    assert_same(o2, w2, a.n_docs, R)
+
+
+def test_exchange_config2_full_size(eng, torch):
+    n = 1 << 20
+    A, B = gen_pair(eng, torch, n, 0x5EED)
+    dev = torch.device("cuda:0")
+    oab = OutBuffers(n, 2, 2 * n * 64, device=dev)
+    oba = OutBuffers(n, 2, 2 * n * 64, device=dev)
+    eng.set_max_doc_entries(64)
+    try:
+        eng.exchange_async(A.as_batch(), B.as_batch(), oab, oba)
+        eng.sync()
+    finally:
+        eng.set_max_doc_entries()
+    ha, hb = host_out(A, torch).as_batch(), host_out(B, torch).as_batch()
+    rc, want = oracle.join(ha, hb)
+    assert rc == 0
+    assert_same_all(host_out(oab, torch), want, n, 2)
+    rc, want = oracle.join(hb, ha)
+    assert rc == 0
+    assert_same_all(host_out(oba, torch), want, n, 2)
+
+
+def test_max_doc_entries_promise_is_checked(eng):
+    R = 2
+    dst = batch_of(R, [([(k, 0, 1) for k in range(70)], [1, 0])])
+    src = batch_of(R, [([], [0, 0])])
+    eng.set_max_doc_entries(64)
+    try:
+        with pytest.raises(crdtgpu.CrdtError) as ei:
+            eng.join(dst, src)
+        assert ei.value.code == crdtgpu.CRDT_E_INVALID
+    finally:
+        eng.set_max_doc_entries()
+    rc, want = oracle.join(dst, src)
+    assert_same(eng.join(dst, src), want, 1, R)

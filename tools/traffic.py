@@ -40,6 +40,8 @@ def main():
     ap.add_argument("dir")
     ap.add_argument("--docs", type=int, default=1 << 20)
     ap.add_argument("--emit", action="store_true")
+    ap.add_argument("--config", type=int, default=2)
+    ap.add_argument("--kernel", default="join_wave_kernel")
     a = ap.parse_args()
     out, calib = {}, {}
     for sub in sorted(os.listdir(a.dir)):
@@ -59,9 +61,10 @@ def main():
     N = 64 << 20
     fcorr = (16 * N) / (cal["FETCH_SIZE"] * 1024) if cal.get("FETCH_SIZE") else None
     wcorr = (8 * N) / (cal["WRITE_SIZE"] * 1024) if cal.get("WRITE_SIZE") else None
-    jk = next((k for k in out if k.startswith("join_wave_kernel")), "")
+    jk = next((k for k in out if k.startswith(a.kernel)), "")
     j = out.get(jk, {})
-    res = {"docs": a.docs, "kernel": jk, "fetch_correction": fcorr, "write_correction": wcorr}
+    res = {"docs": a.docs, "config": a.config, "kernel": jk, "exchange": jk.endswith("true>"),
+           "fetch_correction": fcorr, "write_correction": wcorr}
     if j.get("FETCH_SIZE") is not None and j.get("WRITE_SIZE") is not None:
         rd = j["FETCH_SIZE"] * 1024 * (fcorr or 1.0)
         wr = j["WRITE_SIZE"] * 1024 * (wcorr or 1.0)
