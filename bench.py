@@ -89,35 +89,31 @@ class Config2:
         self.ctx_ba = torch.zeros(R, dtype=torch.int64, device=dev)
         self.a, self.b = self.A.as_batch(), self.B.as_batch()
         self.merges_per_step = 2 * n
-        self.n_events = 3
 
-    def step(self, ev=None):
-        """A <- B and B <- A for every doc; returns the local causal-context summary."""
-        s, eng, n, R = self.stream, self.eng, self.n, self.R
-        if ev is not None:
-            ev[0].record(s)
+    def _structs(self):
+        if not hasattr(self, "_cs"):
+            self._cs = (self.a.c(), self.b.c(), self.oab.c(), self.oba.c())
+        return self._cs
+
+    def hot(self, s):
+        """The dominant launch(es): A <- B and B <- A for every doc."""
+        ca, cb, cab, cba = self._structs()
         if self.exchange:
-            eng.exchange_async(self.a, self.b, self.oab, self.oba, stream=s)
+            self.eng.exchange_async(ca, cb, cab, cba, stream=s)
         else:
-            eng.join_async(self.a, self.b, self.oab, stream=s)
-        if ev is not None:
-            ev[1].record(s)
-        if not self.exchange:
-            eng.join_async(self.b, self.a, self.oba, stream=s)
-        if ev is not None:
-            ev[2].record(s)
+            self.eng.join_async(ca, cb, cab, stream=s)
+            self.eng.join_async(cb, ca, cba, stream=s)
+
+    def post(self, s):
+        """Per-GPU causal-context summary of the outputs; returns the R-vector."""
+        eng, n, R = self.eng, self.n, self.R
         eng.causal_context_async(self.oab.vv, n, R, self.ctx_ab, stream=s)
         eng.causal_context_async(self.oba.vv, n, R, self.ctx_ba, stream=s)
         eng.vv_max_async(self.ctx_ab, self.ctx_ba, R, stream=s)
         return self.ctx_ab
 
-    def launch_seconds(self, events, steps):
-        """Mean duration of one launch of the dominant kernel (exchange: the one launch)."""
-        t_ab = sum(e[0].elapsed_time(e[1]) for e in events) / steps / 1e3
-        if self.exchange:
-            return t_ab
-        t_ba = sum(e[1].elapsed_time(e[2]) for e in events) / steps / 1e3
-        return (t_ab + t_ba) / 2
+    def launches_per_step(self):
+        return 1 if self.exchange else 2
 
     def bytes_per_launch(self):
         """SURVEY 8d per-merge bytes x the merges one launch performs (exchange: 2 per doc)."""
@@ -156,7 +152,7 @@ class Config2:
                           "(no Go toolchain on the box: the reference itself cannot run)" % (n_sample, merges, el)}
 
 
-class Config4:
+class Config4(Config2):
     """Skewed sizes (Zipf(1.1)-like, up to 2^20 entries) with 50% concurrent
     add/remove conflicts, full-state join both directions (BASELINE configs[3])."""
 
@@ -188,12 +184,7 @@ class Config4:
         self.ctx_ba = torch.zeros(R, dtype=torch.int64, device=dev)
         self.a, self.b = self.A.as_batch(), self.B.as_batch()
         self.merges_per_step = 2 * n
-        self.n_events = 3
         self.sizes = sizes
-
-    step = Config2.step
-    launch_seconds = Config2.launch_seconds
-    bytes_per_launch = Config2.bytes_per_launch
 
     def describe(self, world):
         return {"workload": "config4: %d docs/GPU, Zipf(1.1)-like sizes in [1, 2^20) (mean %.0f, max %d, %d entries "
@@ -242,22 +233,20 @@ class Config3:
         self.ctx = torch.zeros(R, dtype=torch.int64, device=dev)
         self.d = self.D.as_batch()
         self.merges_per_step = n * M
-        self.n_events = 2
 
-    def step(self, ev=None):
-        import crdtgpu
+    mode = 1  # CRDT_FOLD_DELTA
 
-        s = self.stream
-        if ev is not None:
-            ev[0].record(s)
-        self.eng.fold_async(crdtgpu.CRDT_FOLD_DELTA, self.d, self.S, self.out, stream=s)
-        if ev is not None:
-            ev[1].record(s)
+    def hot(self, s):
+        if not hasattr(self, "_cs"):
+            self._cs = (self.d.c(), self.S.c(), self.out.c())
+        self.eng.fold_async(self.mode, *self._cs, stream=s)
+
+    def post(self, s):
         self.eng.causal_context_async(self.out.vv, self.n, self.R, self.ctx, stream=s)
         return self.ctx
 
-    def launch_seconds(self, events, steps):
-        return sum(e[0].elapsed_time(e[1]) for e in events) / steps / 1e3
+    def launches_per_step(self):
+        return 1
 
     def bytes_per_launch(self):
         from crdtgpu import workloads
@@ -326,22 +315,11 @@ class Config5:
         self.ctx = torch.zeros(R, dtype=torch.int64, device=dev)
         self.d = self.D.as_batch()
         self.merges_per_step = n * (P - 1)
-        self.n_events = 2
 
-    def step(self, ev=None):
-        import crdtgpu
-
-        s = self.stream
-        if ev is not None:
-            ev[0].record(s)
-        self.eng.fold_async(crdtgpu.CRDT_FOLD_AWSET, self.d, self.S, self.out, stream=s)
-        if ev is not None:
-            ev[1].record(s)
-        self.eng.causal_context_async(self.out.vv, self.n, self.R, self.ctx, stream=s)
-        return self.ctx
-
-    def launch_seconds(self, events, steps):
-        return sum(e[0].elapsed_time(e[1]) for e in events) / steps / 1e3
+    mode = 0  # CRDT_FOLD_AWSET
+    hot = Config3.hot
+    post = Config3.post
+    launches_per_step = Config3.launches_per_step
 
     def bytes_per_launch(self):
         from crdtgpu import workloads
@@ -394,7 +372,8 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--separate", action="store_true", help="configs 2/4: two join launches instead of one exchange")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"))
+    ap.add_argument("--no-graph", action="store_true", help="launch eagerly instead of replaying a captured HIP graph")
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
     args = ap.parse_args()
 
     import numpy as np
@@ -426,8 +405,28 @@ def main():
     W = cls(eng, n, seed, dev, stream)
     eng.sync(stream)
 
+    # The dominant launch is captured once into a HIP graph and replayed each
+    # step: one host call per step instead of the ctypes/ABI calls of every
+    # kernel, so a loaded host cannot stretch the step.
+    graph = None
+    if not args.no_graph:
+        W.hot(stream)  # warm the workspaces before capture (no allocation inside)
+        torch.cuda.synchronize()
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            W.hot(torch.cuda.current_stream())
+        torch.cuda.synchronize()
+
     def step(ev=None):
-        local_ctx = W.step(ev)
+        if ev is not None:
+            ev[0].record(stream)
+        if graph is not None:
+            graph.replay()
+        else:
+            W.hot(stream)
+        if ev is not None:
+            ev[1].record(stream)
+        local_ctx = W.post(stream)
         if dist is not None:
             return u64_max_allreduce(dist, local_ctx)
         return local_ctx
@@ -437,7 +436,7 @@ def main():
     eng.sync(stream)
     bytes_launch = W.bytes_per_launch()  # algorithmic bytes from the actual output sizes
 
-    events = [[torch.cuda.Event(enable_timing=True) for _ in range(W.n_events)] for _ in range(args.steps)]
+    events = [[torch.cuda.Event(enable_timing=True) for _ in range(2)] for _ in range(args.steps)]
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
@@ -455,18 +454,20 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    t_launch = W.launch_seconds(events, args.steps)
+    # mean duration of one launch of the dominant kernel, HIP events on its stream
+    t_launch = sum(e[0].elapsed_time(e[1]) for e in events) / args.steps / 1e3 / W.launches_per_step()
     achieved = bytes_launch / t_launch / 1e9
     global_ctx = g.cpu().numpy().view(np.uint64).tolist() if g is not None else []
 
+    # HBM bytes per launch of this kernel from the PMC passes (tools/pmc.sh ->
+    # tools/traffic.py --emit), matched on config, docs and kernel instance
     traffic = None
     if os.path.exists(args.traffic_json):
         try:
-            tj = json.load(open(args.traffic_json))
-            if (tj.get("docs") == n and tj.get("kernel", "").startswith(W.kernel)
-                    and bool(tj.get("exchange", False)) == bool(getattr(W, "exchange", False))
-                    and tj.get("config", 2) == args.config):
-                traffic = tj.get("hbm_bytes_per_launch")
+            for e in json.load(open(args.traffic_json)):
+                if (e.get("docs") == n and e.get("config") == args.config and e.get("kernel", "").startswith(W.kernel)
+                        and bool(e.get("exchange")) == bool(getattr(W, "exchange", False))):
+                    traffic = e.get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
 
@@ -484,6 +485,7 @@ def main():
         "vs_baseline": None,
         "dtype": "u64",
         "data": "synthetic (AWSet states generated on device, csrc/gen.hip)",
+        "launch": "hip graph replay" if graph is not None else "eager",
         "config": W.describe(world),
         "roofline": {
             "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",

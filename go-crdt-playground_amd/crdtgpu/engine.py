@@ -9,6 +9,12 @@ from .abi import check
 from .batch import AWSetBatch, OutBuffers, SrcBatch, ptr
 
 
+def _c(x):
+    """ctypes struct of a batch/output (or the struct itself, prebuilt by the caller
+    to keep per-launch host work at a few ctypes calls)."""
+    return x.c() if hasattr(x, "c") else x
+
+
 def _stream(stream):
     if stream is None:
         return None
@@ -57,17 +63,17 @@ class Engine:
 
     # -- device-resident, asynchronous -------------------------------------
     def join_async(self, dst: AWSetBatch, src: AWSetBatch, out: OutBuffers, stream=None):
-        d, s, o = dst.c(), src.c(), out.c()
+        d, s, o = _c(dst), _c(src), _c(out)
         check(self._lib.crdt_awset_join_async(self._ctx, ctypes.byref(d), ctypes.byref(s), ctypes.byref(o),
                                               _stream(stream)), "crdt_awset_join_async")
 
     def exchange_async(self, a: AWSetBatch, b: AWSetBatch, out_ab: OutBuffers, out_ba: OutBuffers, stream=None):
-        ca, cb, o1, o2 = a.c(), b.c(), out_ab.c(), out_ba.c()
+        ca, cb, o1, o2 = _c(a), _c(b), _c(out_ab), _c(out_ba)
         check(self._lib.crdt_awset_exchange_async(self._ctx, ctypes.byref(ca), ctypes.byref(cb), ctypes.byref(o1),
                                                   ctypes.byref(o2), _stream(stream)), "crdt_awset_exchange_async")
 
     def fold_async(self, mode: int, dst: AWSetBatch, srcs: SrcBatch, out: OutBuffers, stream=None):
-        d, s, o = dst.c(), srcs.c(), out.c()
+        d, s, o = _c(dst), _c(srcs), _c(out)
         check(self._lib.crdt_awset_fold_async(self._ctx, int(mode), ctypes.byref(d), ctypes.byref(s),
                                               ctypes.byref(o), _stream(stream)), "crdt_awset_fold_async")
 

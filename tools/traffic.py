@@ -6,7 +6,7 @@ FETCH_SIZE + WRITE_SIZE (KiB units), corrected by the known-byte calibration run
 (tools/calib.py: vv_max_kernel, 8 B per lane): correction = known bytes /
 counted bytes, applied per direction (the guide's gfx950 note: FETCH_SIZE counts
 half of a wide coalesced stream; other widths must be calibrated).
-Writes <dir>/traffic.json and, with --emit, profiles/traffic_latest.json.
+Writes <dir>/traffic.json and, with --emit, adds the entry to profiles/traffic.json.
 """
 import argparse
 import csv
@@ -73,7 +73,12 @@ def main():
     print(json.dumps(res, indent=1))
     json.dump(res, open(os.path.join(a.dir, "traffic.json"), "w"), indent=1)
     if a.emit:
-        json.dump(res, open("profiles/traffic_latest.json", "w"), indent=1)
+        # profiles/traffic.json: one entry per (config, docs, kernel); bench.py picks its own
+        path = "profiles/traffic.json"
+        table = json.load(open(path)) if os.path.exists(path) else []
+        table = [e for e in table if (e["config"], e["docs"], e["kernel"]) != (res["config"], res["docs"], res["kernel"])]
+        table.append(res)
+        json.dump(table, open(path, "w"), indent=1)
 
 
 if __name__ == "__main__":
