@@ -70,6 +70,7 @@ class Config2:
     metric = "replica-merges/sec (AWSet full-state join) + achieved HBM GB/s (% roofline)"
 
     exchange = True  # both directions from one read (crdt_awset_exchange_async); --separate: two joins
+    graph_ok = True  # hot() is one kernel launch, replayed from a captured HIP graph (validated on MI355X)
 
     def __init__(self, eng, n, seed, dev, stream):
         import torch
@@ -158,6 +159,7 @@ class Config4(Config2):
 
     R = 2
     kernel = "join_block_kernel"
+    graph_ok = False  # worklist path (several kernels): eager launches
     metric = "replica-merges/sec (AWSet join, Zipf sizes, config 4) + achieved HBM GB/s (% roofline)"
 
     def __init__(self, eng, n, seed, dev, stream):
@@ -235,6 +237,7 @@ class Config3:
         self.merges_per_step = n * M
 
     mode = 1  # CRDT_FOLD_DELTA
+    graph_ok = False  # eager launches (graph replay of the fold path not validated yet)
 
     def hot(self, s):
         if not hasattr(self, "_cs"):
@@ -317,6 +320,7 @@ class Config5:
         self.merges_per_step = n * (P - 1)
 
     mode = 0  # CRDT_FOLD_AWSET
+    graph_ok = False
     hot = Config3.hot
     post = Config3.post
     launches_per_step = Config3.launches_per_step
@@ -409,7 +413,7 @@ def main():
     # step: one host call per step instead of the ctypes/ABI calls of every
     # kernel, so a loaded host cannot stretch the step.
     graph = None
-    if not args.no_graph:
+    if not args.no_graph and W.graph_ok:
         W.hot(stream)  # warm the workspaces before capture (no allocation inside)
         torch.cuda.synchronize()
         graph = torch.cuda.CUDAGraph()

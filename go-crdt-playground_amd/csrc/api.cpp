@@ -17,6 +17,7 @@ hipError_t launch_join(const BatchView& dst, const BatchView& src, const OutView
 hipError_t launch_fold(int mode, const BatchView& dst, const SrcView& sb, const OutView& out, const Scratch& scr,
                        const Work& wk, uint32_t block_grid, hipStream_t stream);
 hipError_t launch_vv_max(uint64_t* dst, const uint64_t* src, size_t n, hipStream_t stream);
+hipError_t launch_reset_work(uint32_t* ws, hipStream_t stream);
 hipError_t launch_context(const uint64_t* vv, uint32_t n_docs, uint32_t R, uint64_t* part, uint32_t n_part,
                           uint64_t* out, hipStream_t stream);
 hipError_t launch_gen_pair(uint64_t seed, uint32_t n_docs, const OutView& A, const OutView& B, hipStream_t stream);
@@ -258,7 +259,7 @@ static int join_common(crdt_ctx* ctx, const crdt_awset_batch* dst, const crdt_aw
     hipStream_t s = (hipStream_t)stream;
     const bool no_large = ctx->max_doc_entries <= 64;
     // the per-call counters are read only by the block path
-    if (!no_large && hipMemsetAsync(ctx->ws.p, 0, 64, s) != hipSuccess) return CRDT_E_HIP;
+    if (!no_large && launch_reset_work(ctx->ws.as<uint32_t>(0), s) != hipSuccess) return CRDT_E_HIP;
     OutView o2v;
     if (out2) o2v = view(out2);
     return hip_err(launch_join(view(dst), view(src), view(out), out2 ? &o2v : nullptr, make_work(ctx),
@@ -286,7 +287,7 @@ int crdt_awset_fold_async(crdt_ctx* ctx, int mode, const crdt_awset_batch* dst, 
     if (rc != CRDT_OK) return rc;
     if (ctx->scratch_slots == 0 && reserve_scratch(ctx, 1) != CRDT_OK) return CRDT_E_NOMEM;
     hipStream_t s = (hipStream_t)stream;
-    if (hipMemsetAsync(ctx->ws.p, 0, 64, s) != hipSuccess) return CRDT_E_HIP;
+    if (launch_reset_work(ctx->ws.as<uint32_t>(0), s) != hipSuccess) return CRDT_E_HIP;
     const size_t slots = ctx->scratch_slots;
     Scratch scr{ctx->scratch.as<uint64_t>(0), ctx->scratch.as<uint32_t>(slots * 16), ctx->scratch.as<uint64_t>(slots * 8),
                 slots};

@@ -200,6 +200,23 @@ __device__ __forceinline__ bool has_dot_bf(const uint64_t* vv, uint32_t R, uint3
     return actor < R && v >= counter;
 }
 
+// Worklist push: the slot and the doc index are checked against the worklist
+// capacity (n_docs), so a counter that was not reset can never turn into an
+// out-of-bounds address -- it surfaces as CRDT_E_WORKSPACE instead.
+__device__ __forceinline__ void push_work(const Work& wk, uint32_t d, uint32_t n_docs) {
+    const uint32_t slot = atomicAdd(wk.wl_count, 1u);
+    if (slot < n_docs)
+        wk.worklist[slot] = d;
+    else
+        atomicOr(wk.status, kErrWorkspace);
+}
+
+// Number of worklist entries a consumer may read (clamped to the capacity).
+__device__ __forceinline__ uint32_t work_total(const Work& wk, uint32_t n_docs) {
+    const uint32_t t = __hip_atomic_load(wk.wl_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return t < n_docs ? t : n_docs;
+}
+
 __device__ __forceinline__ void flag_error(uint32_t* status, uint32_t err) {
     // one atomic per wave that saw an error
     uint64_t m = ballot(err != 0);

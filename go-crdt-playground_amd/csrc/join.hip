@@ -183,7 +183,7 @@ __global__ __launch_bounds__(WAVES * 64) void join_wave_kernel(BatchView dst, Ba
             if (no_large)
                 atomicOr(wk.status, kErrHint);
             else
-                wk.worklist[atomicAdd(wk.wl_count, 1u)] = dd;
+                push_work(wk, dd, n_docs);
         }
     };
 
@@ -238,10 +238,14 @@ __global__ __launch_bounds__(NT) void join_block_kernel(BatchView dst, BatchView
         if (tid == 0) sm.word[0] = atomicAdd(wk.wl_head + head, 1u);
         __syncthreads();
         const uint32_t slot = sm.word[0];
-        const uint32_t total = __hip_atomic_load(wk.wl_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t total = work_total(wk, dst.n_docs);
         __syncthreads();
         if (slot >= total) break;
         const uint32_t d = wk.worklist[slot];
+        if (d >= dst.n_docs) {  // not a document of this call: never dereferenced
+            if (tid == 0) atomicOr(wk.status, kErrWorkspace);
+            continue;
+        }
         const uint32_t doff = dst.offsets[d], soff = src.offsets[d];
         const Entries D{dst.keys + doff, dst.actors + doff, dst.counters + doff, live_count(dst.offsets, dst.counts, d)};
         const Entries S{src.keys + soff, src.actors + soff, src.counters + soff, live_count(src.offsets, src.counts, d)};

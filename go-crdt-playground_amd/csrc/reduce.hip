@@ -74,6 +74,15 @@ __global__ __launch_bounds__(NT) void context_final_kernel(const uint64_t* __res
 
 constexpr int kCtxNT = 256;
 
+// Zero the per-call work counters (workspace words [0, 16)).  A kernel rather
+// than hipMemsetAsync so a captured call is a graph of kernel nodes only.
+__global__ void reset_work_kernel(uint32_t* ws) { ws[threadIdx.x] = 0u; }
+
+hipError_t launch_reset_work(uint32_t* ws, hipStream_t stream) {
+    hipLaunchKernelGGL(reset_work_kernel, dim3(1), dim3(16), 0, stream, ws);
+    return hipGetLastError();
+}
+
 hipError_t launch_vv_max(uint64_t* dst, const uint64_t* src, size_t n, hipStream_t stream) {
     if (n == 0) return hipSuccess;
     size_t grid = (n + 255) / 256;
