@@ -1,0 +1,161 @@
+"""CPU: the per-key restatement of the ordered fold that fold_sort_kernel
+(go-crdt-playground_amd/csrc/fold.hip) implements, checked against the C oracle
+(step-by-step replay of awset.go:103-161 / awset-delta_test.go:51-166) on
+randomized adversarial documents -- tombstones (effective and re-added),
+no-op delta steps, first contact (Counter(src.Actor) == 0), keys known only to
+sources, actor == len(VV) panics and actor > len(VV).
+
+The model follows the kernel's four phases literally (schedule, keep/tag,
+sort by (key, tag), event walk per key), so a pass here says the
+formulation is the reference's semantics, including which HasDot calls can
+panic; the GPU tests then check the kernel against the same oracle."""
+
+import random
+
+import pytest
+
+from crdtgpu import CRDT_FOLD_AWSET, CRDT_FOLD_DELTA
+from crdtgpu.batch import AWSetBatch, SrcBatch
+from oracle import oracle
+
+
+def model_fold(mode, ents, vv0, chain):
+    """Per-key replay of one document; returns (err, entries, vv)."""
+    R = len(vv0)
+    delta = mode == CRDT_FOLD_DELTA
+    err = False
+
+    def has_dot(vv, a, c):
+        nonlocal err
+        if a >= R:
+            err |= a == R  # crdt-misc.go:28-34: vv[a] with a == len panics
+            return False
+        return vv[a] >= c
+
+    # 1. schedule (fold.hip "schedule"): effective tombstones, V_j, full_j, noop_j
+    eff = {}
+    for j, (_, _, e, t) in enumerate(chain):
+        emap = {k: (a, c) for k, a, c in e}
+        for x, (k, a, c) in enumerate(t or []):
+            s = emap.get(k)
+            eff[(j, x)] = not (s is not None and (s[0] != a or s[1] > c))
+    V = list(vv0)
+    Vs, full, noop, chg = [], [], [], {}
+    for j, (aj, svv, e, t) in enumerate(chain):
+        Vs.append(list(V))
+        f = True
+        if delta:
+            if aj == R:
+                err = True
+            f = (V[aj] if aj < R else 0) == 0
+        nop = False
+        if not f:
+            any_chg = False
+            for i, (k, a, c) in enumerate(e):
+                chg[(j, i)] = not has_dot(V, a, c)
+                any_chg |= chg[(j, i)]
+            nop = not any_chg and not any(eff[(j, x)] for x in range(len(t or [])))
+        full.append(f)
+        noop.append(nop)
+        if not nop:
+            V = [max(x, y) for x, y in zip(V, svv)]
+    # 2. keep + tag: (key, tag, actor, counter); tag orders doc < entries < tombstones per step
+    tup = [(k, 0, a, c) for k, a, c in ents]
+    for j, (aj, svv, e, t) in enumerate(chain):
+        if noop[j]:
+            continue
+        for i, (k, a, c) in enumerate(e):
+            if full[j] or chg[(j, i)]:
+                tup.append((k, (j + 1) * 2, a, c))
+        if delta and not full[j]:
+            for x, (k, a, c) in enumerate(t or []):
+                if eff[(j, x)]:
+                    tup.append((k, (j + 1) * 2 + 1, a, c))
+    # 3. group by key in replay order
+    tup.sort(key=lambda z: (z[0], z[1]))
+    segs = {}
+    for z in tup:
+        segs.setdefault(z[0], []).append(z)
+    # 4. event walk per key
+    out = []
+    for key in sorted(segs):
+        ev = segs[key]
+        p, pres, a, c = 0, False, 0, 0
+        if ev[0][1] == 0:
+            pres, a, c = True, ev[0][2], ev[0][3]
+            p = 1
+        jn = 0
+        while True:
+            ts = (ev[p][1] >> 1) - 1 if p < len(ev) else 64
+            nf = next((j for j in range(jn, len(chain)) if full[j]), 64) if pres else 64
+            je = min(ts, nf)
+            if je >= 64:
+                break
+            is_e = is_t = False
+            if ts == je and not ev[p][1] & 1:
+                is_e, ea, ec = True, ev[p][2], ev[p][3]
+                p += 1
+            if delta and p < len(ev) and (ev[p][1] >> 1) - 1 == je:
+                is_t, xa, xc = True, ev[p][2], ev[p][3]
+                p += 1
+            if full[je]:
+                if is_e:
+                    if pres or not has_dot(Vs[je], ea, ec):
+                        pres, a, c = True, ea, ec
+                elif pres and has_dot(chain[je][1], a, c):
+                    pres = False
+            else:
+                if is_e:
+                    pres, a, c = True, ea, ec
+                if is_t and pres and not has_dot(Vs[je], xa, xc):
+                    pres = False
+            jn = je + 1
+        if pres:
+            out.append((key, a, c))
+    return err, out, V
+
+
+def rand_doc(rng, R, mode):
+    U = rng.choice([6, 12, 40])
+
+    def dots(p, amax):
+        return sorted((k, rng.randrange(amax), rng.randint(1, 6)) for k in range(U) if rng.random() < p)
+
+    amax = R + 2 if rng.random() < 0.15 else R  # sometimes actor == R (panic) or > R (never seen)
+    vv0 = [rng.randint(0, 6) for _ in range(R)]
+    if rng.random() < 0.3:
+        vv0[rng.randrange(R)] = 0
+    ents = dots(rng.uniform(0.0, 0.8), amax)
+    chain = []
+    for _ in range(rng.randint(0, 6)):
+        aj = rng.randrange(amax)
+        svv = [rng.randint(0, 8) for _ in range(R)]
+        e = dots(rng.uniform(0.0, 0.6), amax)
+        t = dots(rng.uniform(0.0, 0.4), amax) if mode == CRDT_FOLD_DELTA else []
+        chain.append((aj, svv, e, t))
+    return ents, vv0, chain
+
+
+@pytest.mark.parametrize("mode", [CRDT_FOLD_AWSET, CRDT_FOLD_DELTA])
+@pytest.mark.parametrize("seed", range(6))
+def test_per_key_model_matches_oracle(mode, seed):
+    rng = random.Random(1000 * seed + mode)
+    checked = errs = 0
+    for _ in range(150):
+        R = rng.choice([1, 2, 3, 5])
+        ents, vv0, chain = rand_doc(rng, R, mode)
+        dst = AWSetBatch.from_docs(R, [(ents, vv0)])
+        srcs = SrcBatch.from_lists(R, [[(a, v, e, t) for a, v, e, t in chain]])
+        rc, want = oracle.fold(mode, dst, srcs)
+        err, got, vv = model_fold(mode, ents, vv0, chain)
+        assert err == (rc != 0), (ents, vv0, chain)
+        if rc:
+            errs += 1
+            continue
+        c = int(want.counts[0])
+        o = int(want.offsets[0])
+        exp = list(zip(want.keys[o:o + c].tolist(), want.actors[o:o + c].tolist(), want.counters[o:o + c].tolist()))
+        assert got == exp, (ents, vv0, chain)
+        assert vv == want.vv[:R].tolist()
+        checked += 1
+    assert checked > 50 and errs > 0
