@@ -217,7 +217,7 @@ class Config3:
 
     R = 16
     M = 10
-    kernel = "fold_wave_kernel"
+    kernel = "fold_sort_kernel"
     metric = "replica-merges/sec (AWSetDelta fold, config 3) + achieved HBM GB/s (% roofline)"
 
     def __init__(self, eng, n, seed, dev, stream):
@@ -299,7 +299,7 @@ class Config5:
 
     R = P = 8
     E = 16
-    kernel = "fold_wave_kernel"
+    kernel = "fold_sort_kernel"
     metric = "replica-merges/sec (AWSet fold r0<-..<-r7, config 5) + achieved HBM GB/s (% roofline)"
 
     def __init__(self, eng, n, seed, dev, stream):
