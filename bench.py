@@ -377,6 +377,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--separate", action="store_true", help="configs 2/4: two join launches instead of one exchange")
     ap.add_argument("--no-graph", action="store_true", help="launch eagerly instead of replaying a captured HIP graph")
+    ap.add_argument("--force-graph", action="store_true", help="replay a captured HIP graph for every config")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
     args = ap.parse_args()
 
@@ -413,7 +414,7 @@ def main():
     # step: one host call per step instead of the ctypes/ABI calls of every
     # kernel, so a loaded host cannot stretch the step.
     graph = None
-    if not args.no_graph and W.graph_ok:
+    if not args.no_graph and (W.graph_ok or args.force_graph):
         W.hot(stream)  # warm the workspaces before capture (no allocation inside)
         torch.cuda.synchronize()
         graph = torch.cuda.CUDAGraph()
@@ -453,6 +454,15 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     eng.sync(stream)
+    replay_check = None
+    if graph is not None and hasattr(W, "out"):
+        # graph-replayed output vs an eager launch of the same call (bitwise)
+        snap = [t.clone() for t in (W.out.counts, W.out.keys, W.out.actors, W.out.counters, W.out.vv)]
+        W.hot(stream)
+        eng.sync(stream)
+        replay_check = all(bool(torch.equal(a, b)) for a, b in
+                           zip(snap, (W.out.counts, W.out.keys, W.out.actors, W.out.counters, W.out.vv)))
+        del snap
     if dist is not None:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -497,6 +507,7 @@ def main():
             "algorithmic_bytes_per_launch": bytes_launch, "launch_ms": t_launch * 1e3,
         },
         "global_causal_context": global_ctx,
+        "replay_check": replay_check,
     }
     if traffic:
         result["roofline"]["traffic_gbs"] = traffic / t_launch / 1e9

@@ -244,6 +244,7 @@ int crdt_ctx_sync(crdt_ctx* ctx, void* stream) {
         if (status & kErrActorRange) return CRDT_E_ACTOR_RANGE;
         if (status & kErrWorkspace) return CRDT_E_WORKSPACE;
         if (status & kErrHint) return CRDT_E_INVALID;
+        if (status & kErrCapacity) return CRDT_E_CAPACITY;
     }
     return CRDT_OK;
 }

@@ -18,6 +18,7 @@ constexpr int kWave = 64;
 constexpr uint32_t kErrActorRange = 1u;
 constexpr uint32_t kErrWorkspace = 2u;  // fold scratch smaller than the output slots
 constexpr uint32_t kErrHint = 4u;       // a doc broke the crdt_ctx_set_max_doc_entries promise
+constexpr uint32_t kErrCapacity = 8u;   // a doc's live count exceeds its slots (clamped)
 
 // Kernel-side view of an AWSet batch (same fields as crdt_awset_batch).
 struct BatchView {
@@ -218,14 +219,49 @@ __device__ __forceinline__ uint32_t work_total(const Work& wk, uint32_t n_docs) 
 }
 
 __device__ __forceinline__ void flag_error(uint32_t* status, uint32_t err) {
-    // one atomic per wave that saw an error
-    uint64_t m = ballot(err != 0);
-    if (m) {
+    // OR of every lane's bits, one atomic per wave that saw an error
+    if (ballot(err != 0)) {
         uint32_t e = err;
-        // OR across the wave via readlane of the first erring lane is enough:
-        // only one error kind exists.
-        if (lane_id() == (uint32_t)__builtin_ctzll(m)) atomicOr(status, e);
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) e |= (uint32_t)__shfl_xor((int)e, o);
+        if (lane_id() == 0) atomicOr(status, e);
     }
 }
+
+// ---- diagnostic phase stamps (tools/fold_probe.hip builds with
+// CRDT_STAMPS; the product library never does).  Each wave sums the cycles
+// between consecutive STAMP(i) points into scalar accumulators and lane 0
+// adds them to g_stamps once at the end (cdna_hip_programming.md s7 stamps).
+#ifdef CRDT_STAMPS
+__device__ unsigned long long g_stamps[16];
+__device__ __forceinline__ uint64_t stamp_now() {
+    uint64_t t;
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    __builtin_amdgcn_sched_barrier(0);
+    return t;
+}
+#define STAMP_DECL                    \
+    uint64_t st_acc[16] = {0};        \
+    uint64_t st_prev = stamp_now();
+#define STAMP(i)                      \
+    {                                 \
+        const uint64_t t_ = stamp_now(); \
+        st_acc[i] += t_ - st_prev;    \
+        st_prev = t_;                 \
+    }
+#define STAMP_PARAM , uint64_t(&st_acc)[16], uint64_t& st_prev
+#define STAMP_ARGS , st_acc, st_prev
+#define STAMP_FLUSH                                                          \
+    if ((threadIdx.x & 63) == 0)                                             \
+        for (int i_ = 0; i_ < 16; ++i_)                                      \
+            if (st_acc[i_]) atomicAdd(&g_stamps[i_], (unsigned long long)st_acc[i_]);
+#else
+#define STAMP_PARAM
+#define STAMP_ARGS
+#define STAMP_DECL
+#define STAMP(i)
+#define STAMP_FLUSH
+#endif
 
 }  // namespace crdt

@@ -9,54 +9,63 @@
 // Steps into one document are applied in order: the
 // document stays on chip for the whole fold and is written to HBM once.
 //
-//  * fold_sort_kernel: one wavefront per document while document + source
-//    entries + tombstones fit 256 tuples (<= 64 sources, sources x R <= 256
-//    clock words).  The fold is replayed per key (see below), not per step.
+//  * fold_pipe_kernel: one wavefront per run of K consecutive documents, while
+//    a document + its source entries + tombstones fit 256 tuples (<= 64
+//    sources, sources x R <= 256 clock words).  The fold is replayed per key
+//    (below), not per step, and the next document's loads are in flight while
+//    the current one is folded.
 //  * fold_block_kernel: every other document (worklist); persistent
 //    workgroups, merge-path walk per step (merge_block.hpp), ping-pong
 //    between the output slots and a scratch copy.
 #include "crdt_device.hpp"
 #include "merge_block.hpp"
+#include "wave_sort.hpp"
 
 namespace crdt {
 
-// ---- fold_sort_kernel: the fold restated per key --------------------------
+// ---- the fold restated per key ---------------------------------------------
 // A key's fate over the whole fold depends only on its own tuples (its dot in
 // the document, its entry in each source, its tombstone in each source) and on
 // three per-step facts of the document: V_j, the clock before step j; full_j,
 // the awset path (or Counter(src.Actor) == 0, awset-delta_test.go:53); noop_j,
 // a delta step with nothing changed and nothing deleted (:60, no VV merge).
-// V_j/full_j/noop_j need only the clocks and one "anything changed?" ballot
-// per step.  So one wavefront per document:
-//   1. schedule  V_j, full_j, noop_j for j < M; mark the tuples that can act
-//                on their key (entries of full steps, changed entries and
-//                effective tombstones of delta steps);
-//   2. group     those tuples by (key, step, kind): a bitonic network held in
-//                registers, EPL tuples per lane, cross-lane stages by lane
-//                shuffles;
-//   3. walk      one lane per distinct key replays its events in step order
-//                (its tuples, and -- while present -- every full step, whose
-//                phase 2 may remove it: awset.go:147-158);
-//   4. write     the survivors, already in key order, ballot-compacted.
-// Work per document is a few ballots per step plus one sort of <= 256 tuples,
-// instead of one sorted merge (binary searches, barriers) per step.
-struct FoldSortSmem {
+//
+// Schedule.  U_j = V_0 max svv_0 max ... max svv_{j-1} (a prefix max, one lane
+// per actor) equals V_j as long as no step is a no-op: if no step is a no-op
+// under U, then by induction on j every V_j = U_j, so full_j, the changed bits
+// and every clock computed from U are the exact ones.  Otherwise (rare: a
+// delta that brings nothing) the steps are replayed one at a time.
+//
+// Per document, one wavefront:
+//   stage     the tuples (loaded while the previous document was folded) -> LDS
+//   schedule  U_j, full_j; changed entries and effective tombstones; no-op check
+//   keep      the tuples that can act on their key (document entries, entries
+//             of full steps, changed entries and effective tombstones of delta
+//             steps), tagged (step, kind), ballot-compacted
+//   group     a bitonic network over (key, tag) in registers (wave_sort.hpp:
+//             DPP and permlane lane exchanges, no LDS)
+//   walk      one lane per distinct key replays its events in step order (its
+//             tuples and, while present, every full step, whose phase 2 may
+//             remove it: awset.go:147-158)
+//   write     the survivors, already in key order, ballot-compacted.  Every
+//             store is issued unconditionally (out-of-range offsets where there
+//             is nothing to write), so the count of memory operations after the
+//             next document's prefetch is fixed and its wait is an exact vmcnt.
+struct FoldSmem {
     static constexpr int NCAP = 256;  // document entries + source entries + tombstones
     static constexpr int VCAP = 256;  // sources x R clock words
     static constexpr int MCAP = 64;   // sources per document
-    uint64_t tk[NCAP];      // tuple keys; after the sort: the key of each segment
-    uint64_t tc[NCAP];      // tuple counters (document, entries, tombstones)
-    uint32_t ta[NCAP];      // tuple actors
-    uint16_t stag[NCAP];    // kept tuples' tags, then the sorted tags
-    uint16_t seg[NCAP + 1]; // first sorted position of each distinct key
-    uint8_t keep[NCAP];     // delta steps: entry changed / tombstone effective
-    uint8_t step[NCAP];     // source index of an entry / tombstone tuple
-    uint64_t vs[VCAP];      // V_j (j < M), R words each
-    uint64_t svv[VCAP];     // source clocks, R words each
-    uint32_t soff[MCAP + 1];
-    uint32_t toff[MCAP + 1];
-    uint32_t sact[MCAP];
-    uint64_t emask;         // steps holding an effective tombstone
+    uint64_t tk[NCAP];        // tuple keys; compacted kept keys; after the sort: segment keys
+    uint64_t tc[NCAP];        // tuple counters
+    uint64_t vs[VCAP];        // V_j (j < M), R words each
+    uint64_t svv[VCAP];       // source clocks, R words each
+    uint32_t ta[NCAP];        // tuple actors
+    uint32_t soff[MCAP + 1];  // source entry ranges, relative to the first source
+    uint32_t sact[MCAP];      // source actors (AWSetDelta.Actor)
+    uint16_t stag[NCAP];      // kept tuples' tags, then the sorted tags
+    uint16_t seg[NCAP + 1];   // first sorted position of each distinct key
+    uint8_t anye[MCAP];       // step j has a changed entry
+    uint8_t anyt[MCAP];       // step j has an effective tombstone
 };
 
 // Tuple tag: bits 15..8 = 0 for a document entry, (j+1)*2 for an entry of
@@ -64,91 +73,54 @@ struct FoldSortSmem {
 // sort order (key, tag) puts a key's tuples in replay order.
 constexpr uint32_t kPadTag = 0xFFFFu;
 
-__device__ __forceinline__ bool tup_less(uint64_t ka, uint32_t ta, uint64_t kb, uint32_t tb) {
-    return ka < kb || (ka == kb && ta < tb);
-}
-
-__device__ __forceinline__ uint64_t shfl_xor64(uint64_t v, int m) {
-    return (uint64_t)__shfl_xor((unsigned long long)v, m);
-}
-
-// Bitonic sort of EPL*64 (key, tag) pairs; element i = lane*EPL + q.
+// Sort the Kc kept (key, tag) pairs of m.tk / m.stag, then record the groups:
+// m.stag = sorted tags, m.seg[s] = first sorted position of distinct key s,
+// m.tk[s] = that key.  Returns the number of distinct keys.
 template <int EPL>
-__device__ __forceinline__ void wave_bitonic(uint64_t (&k)[EPL], uint32_t (&t)[EPL], uint32_t lane) {
-    constexpr int P = EPL * 64;
+__device__ __forceinline__ uint32_t sort_group(FoldSmem& m, uint32_t Kc, uint32_t lane, uint64_t lt) {
+    uint64_t k[EPL];
+    uint32_t t[EPL];
 #pragma unroll
-    for (int kk = 2; kk <= P; kk <<= 1) {
+    for (int q = 0; q < EPL; ++q) {
+        const uint32_t i = lane * EPL + q;
+        k[q] = i < Kc ? m.tk[i] : ~0ull;
+        t[q] = i < Kc ? (uint32_t)m.stag[i] : kPadTag;
+    }
+    wave_sync();
+    wave_sort_pairs<EPL>(k, t, Kc, lane);
+    bool head[EPL];
+    uint32_t pre = 0;
+    const uint32_t U = segment_heads<EPL>(k, t, kPadTag, lane, lt, head, pre);
 #pragma unroll
-        for (int jj = kk >> 1; jj > 0; jj >>= 1) {
-            if (jj >= EPL) {
-                const int lm = jj / EPL;
-                const bool lower = (lane & lm) == 0;
-#pragma unroll
-                for (int q = 0; q < EPL; ++q) {
-                    const bool asc = (((lane * EPL + q) & kk) == 0);
-                    const uint64_t pk = shfl_xor64(k[q], lm);
-                    const uint32_t pt = (uint32_t)__shfl_xor((int)t[q], lm);
-                    const bool take = (lower == asc) ? tup_less(pk, pt, k[q], t[q]) : tup_less(k[q], t[q], pk, pt);
-                    k[q] = take ? pk : k[q];
-                    t[q] = take ? pt : t[q];
-                }
-            } else {
-#pragma unroll
-                for (int q = 0; q < EPL; ++q) {
-                    if (q & jj) continue;
-                    const int r = q | jj;
-                    const bool asc = (((lane * EPL + q) & kk) == 0);
-                    const bool sw = asc ? tup_less(k[r], t[r], k[q], t[q]) : tup_less(k[q], t[q], k[r], t[r]);
-                    const uint64_t k0 = k[q], k1 = k[r];
-                    const uint32_t t0 = t[q], t1 = t[r];
-                    k[q] = sw ? k1 : k0;
-                    k[r] = sw ? k0 : k1;
-                    t[q] = sw ? t1 : t0;
-                    t[r] = sw ? t0 : t1;
-                }
-            }
+    for (int q = 0; q < EPL; ++q) {
+        const uint32_t i = lane * EPL + q;
+        if (i < Kc) m.stag[i] = (uint16_t)t[q];
+        if (head[q]) {
+            m.seg[pre] = (uint16_t)i;
+            m.tk[pre] = k[q];
+            ++pre;
         }
     }
+    if (lane == 0) m.seg[U] = (uint16_t)Kc;
+    wave_sync();
+    return U;
 }
 
-// Load cnt (key, actor, counter) triples from global [o, o+cnt) into LDS at
-// [base, base+cnt), cnt <= 256: all loads first (unused chunks skipped by a
-// uniform branch, lanes past cnt read 0), then the LDS stores.
-__device__ __forceinline__ void load_tuples(FoldSortSmem& m, uint32_t base, const uint64_t* gk, const uint32_t* ga,
-                                            const uint64_t* gc, uint32_t o, uint32_t cnt, uint32_t lane) {
-    const rsrc_t rk = make_rsrc(gk + o, cnt * 8u), ra = make_rsrc(ga + o, cnt * 4u), rc = make_rsrc(gc + o, cnt * 8u);
-    uint64_t kk[4], cc[4];
-    uint32_t aa[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        if (q * 64u >= cnt) break;
-        const uint32_t i = q * 64 + lane;
-        kk[q] = ld64(rk, i * 8u);
-        aa[q] = ld32(ra, i * 4u);
-        cc[q] = ld64(rc, i * 8u);
-    }
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        if (q * 64u >= cnt) break;
-        const uint32_t i = q * 64 + lane;
-        if (i < cnt) {
-            m.tk[base + i] = kk[q];
-            m.ta[base + i] = aa[q];
-            m.tc[base + i] = cc[q];
-        }
-    }
-}
+// (no bool members: a struct copy with padding bytes goes through scratch)
+struct KeyFate {
+    uint64_t key, c;
+    uint32_t a, emit;
+};
 
-// Walk one round of up to 64 keys (segments r0 + lane) and write the survivors.
+// Replay the events of distinct key s (< U) in step order.
 template <bool DELTA>
-__device__ __forceinline__ uint32_t walk_round(FoldSortSmem& m, uint32_t r0, uint32_t U, uint32_t K, uint32_t R,
-                                               uint64_t full_mask, uint32_t lane, uint64_t lt, rsrc_t ok, rsrc_t oa,
-                                               rsrc_t oc, uint32_t carry, uint32_t& err) {
-    const uint32_t s = r0 + lane;
+__device__ __forceinline__ KeyFate walk_key(const FoldSmem& m, uint32_t s, uint32_t U, uint32_t R,
+                                            uint64_t full_mask, uint32_t& err) {
     const bool act = s < U;
     uint32_t p = act ? m.seg[s] : 0u;
     const uint32_t p1 = act ? m.seg[s + 1] : 0u;
-    const uint64_t key = m.tk[act ? s : 0u];
+    KeyFate f;
+    f.key = m.tk[act ? s : 0u];
     uint32_t tg = act ? m.stag[p] : kPadTag;
     bool pres = false;
     uint32_t a = 0;
@@ -190,92 +162,52 @@ __device__ __forceinline__ uint32_t walk_round(FoldSortSmem& m, uint32_t r0, uin
             }
             if (full) {
                 if (is_e) {
-                    // awset.go:117-141: common key -> src dot; src-only -> added iff dst clock lacks it
+                    // awset.go:122-143: common key -> src dot; src-only -> added iff dst clock lacks it
                     if (pres || !has_dot_bf(m.vs + je * R, R, ea, ec, true, err)) {
                         pres = true;
                         a = ea;
                         c = ec;
                     }
                 } else if (pres && has_dot_bf(m.svv + je * R, R, a, c, true, err)) {
-                    pres = false;  // awset.go:150-153: src saw it and dropped it
+                    pres = false;  // awset.go:150-155: src saw it and dropped it
                 }
             } else {
-                if (is_e) {  // changed entry: deltaMerge phase 1 (awset-delta_test.go:126-144)
+                if (is_e) {  // changed entry: deltaMerge phase 1 (awset-delta_test.go:126-147)
                     pres = true;
                     a = ea;
                     c = ec;
                 }
-                // phase 2 (:146-163): an effective tombstone removes a present
+                // phase 2 (:149-164): an effective tombstone removes a present
                 // key unless the clock before this step already holds its dot
                 if (is_t && pres && !has_dot_bf(m.vs + je * R, R, xa, xc, true, err)) pres = false;
             }
             jn = je + 1;
         }
     }
-    const bool emit = act && pres;
-    const uint64_t em = ballot(emit);
-    const uint32_t pos = carry + popc(em & lt);
-    const uint32_t ko = emit ? pos * 8u : kOOB, ao = emit ? pos * 4u : kOOB;
-    st64<kAuxNT>(key, ok, ko);
-    st32<kAuxNT>(a, oa, ao);
-    st64<kAuxNT>(c, oc, ko);
-    return carry + popc(em);
+    f.emit = (act && pres) ? 1u : 0u;
+    f.a = a;
+    f.c = c;
+    return f;
 }
 
-template <int EPL, bool DELTA>
-__device__ __forceinline__ uint32_t sort_and_walk(FoldSortSmem& m, uint32_t K, uint32_t R, uint64_t full_mask,
-                                                  uint32_t lane, uint64_t lt, rsrc_t ok, rsrc_t oa, rsrc_t oc,
-                                                  uint32_t& err) {
-    uint64_t k[EPL];
-    uint32_t t[EPL];
-#pragma unroll
-    for (int q = 0; q < EPL; ++q) {
-        const uint32_t i = lane * EPL + q;
-        k[q] = i < K ? m.tk[i] : ~0ull;
-        t[q] = i < K ? (uint32_t)m.stag[i] : kPadTag;
-    }
-    wave_sync();
-    wave_bitonic<EPL>(k, t, lane);
-    // segment heads: first tuple of each distinct key
-    const uint64_t prev = (uint64_t)__shfl_up((unsigned long long)k[EPL - 1], 1);
-    bool head[EPL];
-    uint32_t hc = 0;
-#pragma unroll
-    for (int q = 0; q < EPL; ++q) {
-        const uint32_t i = lane * EPL + q;
-        const uint64_t pk = q == 0 ? prev : k[q - 1];
-        head[q] = t[q] != kPadTag && (i == 0 || k[q] != pk);
-        hc += head[q];
-    }
-    uint32_t pre = 0, U = 0;
-#pragma unroll
-    for (int b = 0; b < 3; ++b) {
-        const uint64_t mb = ballot((hc >> b) & 1u);
-        pre += popc(mb & lt) << b;
-        U += popc(mb) << b;
-    }
-#pragma unroll
-    for (int q = 0; q < EPL; ++q) {
-        const uint32_t i = lane * EPL + q;
-        if (i < K) m.stag[i] = (uint16_t)t[q];
-        if (head[q]) {
-            m.seg[pre] = (uint16_t)i;
-            m.tk[pre] = k[q];
-            ++pre;
-        }
-    }
-    if (lane == 0) m.seg[U] = (uint16_t)K;
-    wave_sync();
-    uint32_t carry = 0;
-    for (uint32_t r0 = 0; r0 < U; r0 += 64)
-        carry = walk_round<DELTA>(m, r0, U, K, R, full_mask, lane, lt, ok, oa, oc, carry, err);
-    return carry;
-}
+// One document's inputs, loaded a document ahead.
+struct FoldPref {
+    uint64_t k[4], c[4], sv[4], dv;
+    uint32_t a[4], eo, eo2, to, to2, act;
+};
 
-template <int WAVES, bool DELTA>
-__global__ __launch_bounds__(WAVES * 64) void fold_sort_kernel(BatchView dst, SrcView sb, OutView out, Work wk) {
-    using Smem = FoldSortSmem;
-    __shared__ Smem smem[WAVES];
+struct DocMeta {
+    uint32_t d, doff, slots, n, s0, ms, e0, E, t0, X, N, big;
+};
+
+constexpr int kFoldWaves = 2;  // wavefronts per workgroup (independent)
+constexpr int kFoldK = 32;     // consecutive documents per wavefront
+constexpr int kFoldStores = 4 * 3 + 2;  // stores of one document's write-out (walk rounds x 3 + count + VV)
+
+template <int K, bool DELTA>
+__global__ __launch_bounds__(kFoldWaves * 64) void fold_pipe_kernel(BatchView dst, SrcView sb, OutView out, Work wk) {
+    using Smem = FoldSmem;
+    __shared__ Smem smem[kFoldWaves];
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t w = threadIdx.x >> 6;
     Smem& m = smem[w];
@@ -284,165 +216,343 @@ __global__ __launch_bounds__(WAVES * 64) void fold_sort_kernel(BatchView dst, Sr
     const uint64_t lt = low_mask(lane);
     const bool tombs = DELTA && sb.tomb_off != nullptr;
     uint32_t err = 0;
+    STAMP_DECL
 
-    for (uint32_t d0 = blockIdx.x * WAVES + w; d0 < n_docs; d0 += gridDim.x * WAVES) {
-        const uint32_t d = uniform(d0);
-        const uint32_t s0 = sb.doc_srcs[d], s1 = sb.doc_srcs[d + 1];
-        const uint32_t ms = s1 - s0;
-        const uint32_t doff = dst.offsets[d];
-        const uint32_t e0 = sb.entry_off[s0], E = sb.entry_off[s1] - e0;
-        const uint32_t t0 = tombs ? sb.tomb_off[s0] : 0u;
-        const uint32_t X = tombs ? sb.tomb_off[s1] - t0 : 0u;
-        const uint32_t obase = doff + e0;
-        const uint32_t cap = dst.offsets[d + 1] - doff + E;
-        const uint32_t n = live_count(dst.offsets, dst.counts, d);
-        if (lane == 0) {
-            out.offsets[d] = obase;
-            if (d == n_docs - 1) out.offsets[n_docs] = dst.offsets[n_docs] + sb.entry_off[sb.doc_srcs[n_docs]];
-        }
-        const uint32_t N = n + E + X;
-        if (N > Smem::NCAP || ms > Smem::MCAP || ms * R > Smem::VCAP) {  // block path
-            if (lane == 0) push_work(wk, d, n_docs);
-            continue;
-        }
-        // ---- load: document, source entries, tombstones, clocks, offsets, actors
-        load_tuples(m, 0, dst.keys, dst.actors, dst.counters, doff, n, lane);
-        load_tuples(m, n, sb.keys, sb.actors, sb.counters, e0, E, lane);
-        if (X) load_tuples(m, n + E, sb.tkeys, sb.tactors, sb.tcounters, t0, X, lane);
-        {
-            const rsrc_t rv = make_rsrc(sb.vv + (size_t)s0 * R, ms * R * 8u);
-            uint64_t vq[Smem::VCAP / 64];
+    const uint32_t first = uniform((blockIdx.x * kFoldWaves + w) * (uint32_t)K);
+    if (first >= n_docs) return;
+    const uint32_t cnt = min((uint32_t)K, n_docs - first);
+
+    // ---- metadata of the run: lane i <= cnt describes document first + i
+    const uint32_t di = first + min(lane, cnt);
+    const uint32_t mv_ds = sb.doc_srcs[di];
+    const uint32_t mv_off = dst.offsets[di];
+    const uint32_t mv_cnt = dst.counts ? dst.counts[min(di, n_docs - 1u)] : 0u;
+    const uint32_t mv_eo = sb.entry_off[mv_ds];
+    const uint32_t mv_to = tombs ? sb.tomb_off[mv_ds] : 0u;
+    const uint32_t slots_i = (uint32_t)__shfl_down((int)mv_off, 1) - mv_off;
+    uint32_t n_i = dst.counts ? mv_cnt : slots_i;
+    if (lane < cnt && n_i > slots_i) {  // live count beyond the slots: clamped, reported
+        err |= kErrCapacity;
+        n_i = slots_i;
+    }
+    const uint32_t ms_i = (uint32_t)__shfl_down((int)mv_ds, 1) - mv_ds;
+    const uint32_t E_i = (uint32_t)__shfl_down((int)mv_eo, 1) - mv_eo;
+    const uint32_t X_i = (uint32_t)__shfl_down((int)mv_to, 1) - mv_to;
+    const bool big_i = lane < cnt && ((uint64_t)n_i + E_i + X_i > (uint64_t)Smem::NCAP ||
+                                      ms_i > (uint32_t)Smem::MCAP || ms_i * R > (uint32_t)Smem::VCAP);
+    const uint64_t bigm = ballot(big_i);
+    if (big_i) push_work(wk, first + lane, n_docs);
+    {   // output slot bounds of the run's documents (+ the batch end after the last one)
+        const bool wr = lane < cnt || (lane == cnt && first + cnt == n_docs);
+        st32(mv_off + mv_eo, make_rsrc(out.offsets + first, (cnt + 1u) * 4u), wr ? lane * 4u : kOOB);
+    }
+
+    auto rl = [](uint32_t v, uint32_t i) { return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)i); };
+    auto meta = [&](uint32_t k) {
+        DocMeta q;
+        q.d = first + k;
+        q.doff = rl(mv_off, k);
+        q.slots = rl(slots_i, k);
+        q.n = rl(n_i, k);
+        q.s0 = rl(mv_ds, k);
+        q.ms = rl(ms_i, k);
+        q.e0 = rl(mv_eo, k);
+        q.E = rl(E_i, k);
+        q.t0 = rl(mv_to, k);
+        q.X = rl(X_i, k);
+        q.N = q.n + q.E + q.X;
+        q.big = (uint32_t)((bigm >> k) & 1ull);
+        return q;
+    };
+    // Issue every load of document q (no waits): tuples [document | source
+    // entries | tombstones] by per-lane address (lanes past N re-read the last
+    // tuple, so no load is exec-masked), clocks and offsets by buffer loads.
+    auto prefetch = [&](FoldPref& P, const DocMeta& q) {
 #pragma unroll
-            for (int q = 0; q < Smem::VCAP / 64; ++q) vq[q] = ld64(rv, (q * 64 + lane) * 8u);
-            const rsrc_t re = make_rsrc(sb.entry_off + s0, (ms + 1) * 4u);
-            const uint32_t eo = ld32(re, lane * 4u), eo2 = ld32(re, (64 + lane) * 4u);
-            uint32_t to = 0, to2 = 0;
+        for (int c = 0; c < 4; ++c) {
+            if ((uint32_t)c * 64u < q.N) {
+                uint32_t i = c * 64u + lane;
+                i = i < q.N ? i : q.N - 1u;
+                const bool isd = i < q.n, iss = i < q.n + q.E;
+                const size_t idx = isd ? (size_t)q.doff + i
+                                       : (iss ? (size_t)q.e0 + (i - q.n) : (size_t)q.t0 + (i - q.n - q.E));
+                const uint64_t* kb = isd ? dst.keys : (iss ? sb.keys : sb.tkeys);
+                const uint32_t* ab = isd ? dst.actors : (iss ? sb.actors : sb.tactors);
+                const uint64_t* cb = isd ? dst.counters : (iss ? sb.counters : sb.tcounters);
+                P.k[c] = kb[idx];
+                P.a[c] = ab[idx];
+                P.c[c] = cb[idx];
+            }
+        }
+        const rsrc_t rv = make_rsrc(sb.vv + (size_t)q.s0 * R, q.ms * R * 8u);
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+            if ((uint32_t)c * 64u < q.ms * R) P.sv[c] = ld64(rv, (c * 64u + lane) * 8u);
+        P.dv = ld64(make_rsrc(dst.vv + (size_t)q.d * R, R * 8u), lane * 8u);
+        const rsrc_t re = make_rsrc(sb.entry_off + q.s0, (q.ms + 1u) * 4u);
+        P.eo = ld32(re, lane * 4u);
+        if (q.ms >= 64) P.eo2 = ld32(re, (64u + lane) * 4u);
+        if (tombs) {
+            const rsrc_t rt = make_rsrc(sb.tomb_off + q.s0, (q.ms + 1u) * 4u);
+            P.to = ld32(rt, lane * 4u);
+            if (q.ms >= 64) P.to2 = ld32(rt, (64u + lane) * 4u);
+        }
+        P.act = ld32(make_rsrc(sb.src_actor + q.s0, q.ms * 4u), lane * 4u);
+    };
+
+    FoldPref P;
+    P.eo2 = P.to = P.to2 = 0;
+    DocMeta cur = meta(0);
+    if (!cur.big) prefetch(P, cur);
+    {   // As many (out-of-range, no-traffic) stores as a document's write-out
+        // issues, so the loop is entered with the same memory operations
+        // behind the prefetch as every later iteration: the compiler's vmcnt
+        // for the staged registers is then exact on both paths into the loop.
+        const rsrc_t none = make_rsrc(out.counts, 0u);
+#pragma unroll
+        for (int i = 0; i < kFoldStores; ++i) st32(0u, none, kOOB + 4u * i);  // distinct: not merged
+    }
+#pragma unroll 1
+    for (uint32_t k = 0; k < cnt; ++k) {
+        STAMP(15)
+        // ---- stage document k (its loads were issued one document ago)
+        uint64_t vreg = 0;              // lane r < R: V_0[r]
+        uint32_t soffv = 0, toffv = 0;  // lane s: end of source s's entries / tombstones
+        if (!cur.big) {
+            const uint32_t N = cur.N, msR = cur.ms * R;
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                const uint32_t i = c * 64u + lane;
+                if ((uint32_t)c * 64u < N && i < N) {
+                    m.tk[i] = P.k[c];
+                    m.ta[i] = P.a[c];
+                    m.tc[i] = P.c[c];
+                }
+                if ((uint32_t)c * 64u < msR && i < msR) m.svv[i] = P.sv[c];
+            }
+            const uint32_t nso = lane == 63 ? rl(P.eo2, 0) : (uint32_t)__shfl_down((int)P.eo, 1);
+            soffv = nso - cur.e0;
+            if (lane <= cur.ms) m.soff[lane] = P.eo - cur.e0;
+            if (lane == 0 && cur.ms >= 64) m.soff[64] = P.eo2 - cur.e0;
             if (tombs) {
-                const rsrc_t rt = make_rsrc(sb.tomb_off + s0, (ms + 1) * 4u);
-                to = ld32(rt, lane * 4u);
-                to2 = ld32(rt, (64 + lane) * 4u);
+                const uint32_t nto = lane == 63 ? rl(P.to2, 0) : (uint32_t)__shfl_down((int)P.to, 1);
+                toffv = nto - cur.t0;
             }
-            const uint32_t ac = ld32(make_rsrc(sb.src_actor + s0, ms * 4u), lane * 4u);
-#pragma unroll
-            for (int q = 0; q < Smem::VCAP / 64; ++q) m.svv[q * 64 + lane] = vq[q];
-            m.soff[lane] = eo - e0;
-            m.toff[lane] = to - t0;
-            if (lane == 0) {
-                m.soff[64] = eo2 - e0;
-                m.toff[64] = to2 - t0;
-                m.emask = 0;
+            if (lane < cur.ms) {
+                m.sact[lane] = P.act;
+                m.anye[lane] = 0;
+                m.anyt[lane] = 0;
             }
-            m.sact[lane] = ac;
-        }
-        uint64_t vreg = ld64(make_rsrc(dst.vv + (size_t)d * R, R * 8u), lane * 8u);  // lane r: V[r]
-        wave_sync();
-        // ---- source index of every entry / tombstone tuple (lane j fills source j's range)
-        if (lane < ms) {
-            const uint32_t a0 = m.soff[lane], a1 = m.soff[lane + 1];
-            for (uint32_t i = a0; i < a1; ++i) m.step[n + i] = (uint8_t)lane;
-            if (X) {
-                const uint32_t b0 = m.toff[lane], b1 = m.toff[lane + 1];
-                for (uint32_t i = b0; i < b1; ++i) m.step[n + E + i] = (uint8_t)lane;
-            }
+            vreg = P.dv;
         }
         wave_sync();
-        // ---- effective tombstones (MakeDeltaMergeData, awset-delta_test.go:93-104):
-        // not re-added in the same source.  Clock-independent, so all at once.
-        if (X) {
-            uint32_t cmax = 0;  // longest source: search depth
-            for (uint32_t j = lane; j < ms; j += 64) cmax = max(cmax, m.soff[j + 1] - m.soff[j]);
+        STAMP(0)
+        // ---- issue document k+1's loads; they fly while document k is folded
+        DocMeta nxt = cur;
+        nxt.big = 1u;
+        if (k + 1 < cnt) {
+            nxt = meta(k + 1);
+            if (!nxt.big) prefetch(P, nxt);
+        }
+        STAMP(1)
+
+        // ---- fold document k
+        uint64_t vfin = 0, full_mask = 0;
+        uint32_t U = 0;
+        if (!cur.big) {
+            const uint32_t n = cur.n, E = cur.E, N = cur.N, ms = cur.ms;
+            // schedule: U_j, one lane per actor
+            uint64_t v = vreg;
+            for (uint32_t j = 0; j < ms; ++j) {
+                if (lane < R) {
+                    m.vs[j * R + lane] = v;
+                    const uint64_t s = m.svv[j * R + lane];
+                    v = v > s ? v : s;
+                }
+            }
+            vfin = v;
+            wave_sync();
+            full_mask = low_mask(ms);  // AWSet fold: every step is a full merge
+            if (DELTA) {
+                // path select (awset-delta_test.go:53): Counter(src.Actor) of the
+                // clock before the step; actor == len(VV) panics in Go
+                const uint32_t aj = lane < ms ? m.sact[lane] : 0u;
+                if (lane < ms && aj == R) err |= kErrActorRange;
+                const uint64_t cj = (lane < ms && aj < R) ? m.vs[lane * R + aj] : 0ull;
+                full_mask = ballot(lane < ms && cj == 0);
+            }
+            STAMP(2)
+            // classify the tuples: kind, step, changed / effective
+            const uint32_t NQ = (N + 63u) >> 6;
+            uint32_t step[4], rel[4];
+            bool isE[4], isT[4];
 #pragma unroll
-            for (int o = 32; o > 0; o >>= 1) cmax = max(cmax, (uint32_t)__shfl_xor((int)cmax, o));
-            for (uint32_t q = 0; q * 64 < X; ++q) {
-                const uint32_t x = q * 64 + lane;
-                if (x < X) {
-                    const uint32_t ti = n + E + x;
-                    const uint32_t j = m.step[ti];
-                    const uint32_t lo = n + m.soff[j], len = m.soff[j + 1] - m.soff[j];
-                    const uint64_t tkey = m.tk[ti];
-                    uint32_t pos = 0;
-                    for (uint32_t st = 256; st > 0; st >>= 1) {
-                        if (st > cmax) continue;
-                        const bool in = pos + st <= len;
-                        const uint64_t v = m.tk[in ? lo + pos + st - 1 : 0u];
-                        pos += (in && v < tkey) ? st : 0u;
+            for (int c = 0; c < 4; ++c) {
+                const uint32_t i = c * 64u + lane;
+                isE[c] = i >= n && i < n + E;
+                isT[c] = i >= n + E && i < N;
+                rel[c] = isE[c] ? i - n : i - n - E;
+                step[c] = 0;
+            }
+            // step of a source tuple = number of sources whose range ends at or before it
+            const uint32_t c0 = n >> 6;  // first chunk holding a source tuple
+            for (uint32_t s = 0; s < ms; ++s) {
+                const uint32_t se = rl(soffv, s), te = rl(toffv, s);
+#pragma unroll
+                for (int c = 0; c < 4; ++c)
+                    if ((uint32_t)c >= c0 && (uint32_t)c < NQ) step[c] += rel[c] >= (isE[c] ? se : te) ? 1u : 0u;
+            }
+            uint32_t cmax = 0;  // longest source: depth of the re-add search
+            if (DELTA && cur.X) {
+                const uint32_t prv = (uint32_t)__shfl_up((int)soffv, 1);
+                cmax = lane < ms ? soffv - (lane ? prv : 0u) : 0u;
+#pragma unroll
+                for (int o = 32; o > 0; o >>= 1) cmax = max(cmax, (uint32_t)__shfl_xor((int)cmax, o));
+            }
+            uint64_t key[4];
+            uint32_t flag = 0, perr = 0;  // flag bit c: changed entry / effective tombstone
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                key[c] = 0;
+                if ((uint32_t)c < NQ) {
+                    const uint32_t i = c * 64u + lane;
+                    const uint32_t ii = i < N ? i : 0u;
+                    key[c] = m.tk[ii];
+                    const uint32_t a = m.ta[ii];
+                    const uint64_t cc = m.tc[ii];
+                    const uint32_t j = step[c] & 63u;
+                    bool f = false;
+                    if (DELTA && isE[c] && !((full_mask >> j) & 1ull)) {
+                        // MakeDeltaMergeData (:84-92): dst's clock has not seen the entry
+                        if (a == R) perr |= kErrActorRange;
+                        f = !(a < R && m.vs[j * R + a] >= cc);
+                        if (f) m.anye[j] = 1;
                     }
-                    const bool in_s = pos < len && m.tk[lo + pos] == tkey;
-                    const bool eff = !(in_s && (m.ta[lo + pos] != m.ta[ti] || m.tc[lo + pos] > m.tc[ti]));
-                    m.keep[ti] = eff;
-                    if (eff) atomicOr((unsigned long long*)&m.emask, 1ull << j);
+                    if (DELTA && isT[c]) {
+                        // effective: not re-added in the same source (:93-102)
+                        const uint32_t lo = n + m.soff[j], len = m.soff[j + 1] - m.soff[j];
+                        uint32_t pos = 0;
+                        for (uint32_t st = 256; st > 0; st >>= 1) {
+                            if (st > cmax) continue;
+                            const bool in = pos + st <= len;
+                            const uint64_t v2 = m.tk[in ? lo + pos + st - 1 : 0u];
+                            pos += (in && v2 < key[c]) ? st : 0u;
+                        }
+                        const bool in_s = pos < len && m.tk[lo + pos] == key[c];
+                        f = !(in_s && (m.ta[lo + pos] != a || m.tc[lo + pos] > cc));
+                        if (f) m.anyt[j] = 1;
+                    }
+                    flag |= f ? (1u << c) : 0u;
                 }
             }
             wave_sync();
-        }
-        // ---- schedule: V_j, full_j, noop_j (one ballot per delta step)
-        uint64_t full_mask = 0, noop_mask = 0;
-        const uint64_t emask = X ? m.emask : 0ull;
-        for (uint32_t j = 0; j < ms; ++j) {
-            if (lane < R) m.vs[j * R + lane] = vreg;
-            bool full = true;
+            STAMP(3)
+            uint64_t noop_mask = 0;
             if (DELTA) {
-                const uint32_t aj = m.sact[j];
-                // VersionVector.Counter (crdt-misc.go:36-41); actor == len panics
-                if (aj == R) err |= kErrActorRange;
-                const uint64_t cnt = aj < R ? (uint64_t)__shfl((unsigned long long)vreg, (int)aj) : 0ull;
-                full = cnt == 0;
+                const bool nz = lane < ms && !((full_mask >> lane) & 1ull) && !m.anye[lane] && !m.anyt[lane];
+                noop_mask = ballot(nz);
             }
-            bool noop = false;
-            if (!full) {
-                const uint32_t a0 = m.soff[j], a1 = m.soff[j + 1];
-                bool any = false;
-                for (uint32_t b = a0; b < a1; b += 64) {
-                    const uint32_t i = b + lane;
-                    const bool v = i < a1;
-                    const uint32_t ea = v ? m.ta[n + i] : 0u;
-                    const uint64_t ec = v ? m.tc[n + i] : 0ull;
-                    const uint64_t have = (uint64_t)__shfl((unsigned long long)vreg, (int)(ea < R ? ea : 0u));
-                    if (v && ea == R) err |= kErrActorRange;  // HasDot panics (crdt-misc.go:28-34)
-                    const bool chg = v && !(ea < R && have >= ec);
-                    if (v) m.keep[n + i] = chg;
-                    any |= chg;
+            if (DELTA && noop_mask) {
+                // a step brings nothing: replay the schedule step by step with the exact clocks
+                const uint64_t emask = ballot(lane < ms && m.anyt[lane]);
+                v = vreg;
+                full_mask = 0;
+                noop_mask = 0;
+                perr = 0;
+                uint32_t fe = 0;  // changed bits of the entries, rebuilt
+                for (uint32_t j = 0; j < ms; ++j) {
+                    if (lane < R) m.vs[j * R + lane] = v;
+                    const uint32_t aj = uniform(m.sact[j]);
+                    const uint64_t cj = aj < R ? readlane64(v, aj) : 0ull;
+                    const bool full = cj == 0;
+                    bool noop = false;
+                    if (!full) {
+                        bool any = false;
+#pragma unroll
+                        for (int c = 0; c < 4; ++c) {
+                            if ((uint32_t)c < NQ) {
+                                const uint32_t i = c * 64u + lane;
+                                const bool mine = isE[c] && step[c] == j;
+                                const uint32_t a = m.ta[mine ? i : 0u];
+                                const uint64_t cc = m.tc[mine ? i : 0u];
+                                const uint64_t have = (uint64_t)__shfl((unsigned long long)v, (int)(a < R ? a : 0u));
+                                if (mine && a == R) perr |= kErrActorRange;
+                                const bool chg = mine && !(a < R && have >= cc);
+                                fe |= chg ? (1u << c) : 0u;
+                                any |= chg;
+                            }
+                        }
+                        noop = !ballot(any) && !((emask >> j) & 1ull);
+                    }
+                    full_mask |= (uint64_t)full << j;
+                    noop_mask |= (uint64_t)noop << j;
+                    if (!noop && lane < R) {
+                        const uint64_t s = m.svv[j * R + lane];
+                        v = v > s ? v : s;
+                    }
                 }
-                noop = !ballot(any) && !((emask >> j) & 1ull);
+                vfin = v;
+                // entries take their rebuilt bits, tombstones keep their effective bits
+                uint32_t tb = 0;
+#pragma unroll
+                for (int c = 0; c < 4; ++c) tb |= isT[c] ? (flag & (1u << c)) : 0u;
+                flag = fe | tb;
+                wave_sync();
             }
-            full_mask |= (uint64_t)full << j;
-            noop_mask |= (uint64_t)noop << j;
-            if (!noop && lane < R) vreg = max(vreg, m.svv[j * R + lane]);
+            err |= perr;
+            // keep + tag, compacted in place over m.tk (every read of m.tk is done)
+            uint32_t Kc = 0;
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                if ((uint32_t)c < NQ) {
+                    const uint32_t i = c * 64u + lane;
+                    const uint32_t j = step[c] & 63u;
+                    const bool fj = (full_mask >> j) & 1ull, nj = (noop_mask >> j) & 1ull;
+                    const bool f = (flag >> c) & 1u;
+                    const bool kept =
+                        (i < n) || (isE[c] && !nj && (fj || f)) || (DELTA && isT[c] && !nj && !fj && f);
+                    const uint32_t tag =
+                        (isE[c] || isT[c]) ? ((((j + 1u) * 2u + (isT[c] ? 1u : 0u)) << 8) | i) : i;
+                    const uint64_t km = ballot(kept);
+                    const uint32_t pos = Kc + popc(km & lt);
+                    if (kept) {
+                        m.tk[pos] = key[c];
+                        m.stag[pos] = (uint16_t)tag;
+                    }
+                    Kc += popc(km);
+                }
+            }
+            wave_sync();
+            STAMP(4)
+            U = Kc <= 64 ? sort_group<1>(m, Kc, lane, lt)
+                         : (Kc <= 128 ? sort_group<2>(m, Kc, lane, lt) : sort_group<4>(m, Kc, lane, lt));
+            STAMP(5)
         }
-        wave_sync();
-        // ---- keep only tuples that act on their key; stage (key, tag) compacted
-        uint32_t K = 0;
-        for (uint32_t q = 0; q * 64 < N; ++q) {
-            const uint32_t i = q * 64 + lane;
-            bool kept = i < N;
-            uint32_t tag = i;
-            const uint64_t key = m.tk[kept ? i : 0u];
-            if (kept && i >= n) {
-                const uint32_t j = m.step[i];
-                const bool tomb = i >= n + E;
-                const bool full = (full_mask >> j) & 1ull;
-                kept = !((noop_mask >> j) & 1ull) && (tomb ? (!full && m.keep[i]) : (full || m.keep[i]));
-                tag |= (((j + 1) * 2 + (tomb ? 1u : 0u)) << 8);
-            }
-            const uint64_t km = ballot(kept);
-            const uint32_t pos = K + popc(km & lt);
-            if (kept) {
-                m.tk[pos] = key;
-                m.stag[pos] = (uint16_t)tag;
-            }
-            K += popc(km);
+        // ---- walk the keys and write the survivors (every store unconditional)
+        const uint32_t obase = cur.doff + cur.e0;
+        const uint32_t capo = cur.big ? 0u : min(cur.slots + cur.E, (uint32_t)Smem::NCAP);
+        const rsrc_t ok = make_rsrc(out.keys + obase, capo * 8u), oa = make_rsrc(out.actors + obase, capo * 4u),
+                     oc = make_rsrc(out.counters + obase, capo * 8u);
+        uint32_t carry = 0;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            KeyFate f{0ull, 0ull, 0u, 0u};
+            if (!cur.big && (uint32_t)r * 64u < U) f = walk_key<DELTA>(m, r * 64u + lane, U, R, full_mask, err);
+            const uint64_t em = ballot(f.emit);
+            const uint32_t pos = carry + popc(em & lt);
+            carry += popc(em);
+            const uint32_t o8 = f.emit ? pos * 8u : kOOB, o4 = f.emit ? pos * 4u : kOOB;
+            st64<kAuxNT>(f.key, ok, o8);
+            st32<kAuxNT>(f.a, oa, o4);
+            st64<kAuxNT>(f.c, oc, o8);
         }
+        st32(carry, make_rsrc(out.counts + cur.d, cur.big ? 0u : 4u), lane == 0 ? 0u : kOOB);
+        st64(vfin, make_rsrc(out.vv + (size_t)cur.d * R, cur.big ? 0u : R * 8u), lane * 8u);
         wave_sync();
-        // ---- sort, walk, write
-        const uint32_t oc_n = cap < Smem::NCAP ? cap : Smem::NCAP;  // survivors <= n + E <= 256
-        const rsrc_t ok = make_rsrc(out.keys + obase, oc_n * 8u), oa = make_rsrc(out.actors + obase, oc_n * 4u),
-                     oc = make_rsrc(out.counters + obase, oc_n * 8u);
-        const uint32_t cnt = K <= 128 ? sort_and_walk<2, DELTA>(m, K, R, full_mask, lane, lt, ok, oa, oc, err)
-                                      : sort_and_walk<4, DELTA>(m, K, R, full_mask, lane, lt, ok, oa, oc, err);
-        if (lane == 0) out.counts[d] = cnt;
-        if (lane < R) out.vv[(size_t)d * R + lane] = vreg;
-        wave_sync();
+        STAMP(6)
+        cur = nxt;
     }
+    STAMP_FLUSH
     flag_error(wk.status, err);
 }
 
@@ -467,8 +577,9 @@ __global__ __launch_bounds__(NT) void fold_block_kernel(int mode, BatchView dst,
         }
         const uint32_t s0 = sb.doc_srcs[d], s1 = sb.doc_srcs[d + 1];
         const uint32_t doff = dst.offsets[d];
+        const uint32_t dslots = dst.offsets[d + 1] - doff;
         const uint32_t obase = doff + sb.entry_off[s0];
-        const uint64_t cap = (uint64_t)(dst.offsets[d + 1] - doff) + (sb.entry_off[s1] - sb.entry_off[s0]);
+        const uint64_t cap = (uint64_t)dslots + (sb.entry_off[s1] - sb.entry_off[s0]);
         if ((uint64_t)obase + cap > scr.slots) {  // crdt_ctx_reserve was not told enough slots
             if (tid == 0) atomicOr(wk.status, kErrWorkspace);
             __syncthreads();
@@ -476,7 +587,9 @@ __global__ __launch_bounds__(NT) void fold_block_kernel(int mode, BatchView dst,
         }
         const EntriesOut O{out.keys + obase, out.actors + obase, out.counters + obase};
         const EntriesOut X{scr.keys + obase, scr.actors + obase, scr.counters + obase};
-        Entries cur{dst.keys + doff, dst.actors + doff, dst.counters + doff, live_count(dst.offsets, dst.counts, d)};
+        const uint32_t live = live_count(dst.offsets, dst.counts, d);
+        if (live > dslots && tid == 0) atomicOr(wk.status, kErrCapacity);
+        Entries cur{dst.keys + doff, dst.actors + doff, dst.counters + doff, live < dslots ? live : dslots};
         int where = 0;  // 0 = input, 1 = out, 2 = scratch
         if (tid < R) sm.dvv[tid] = dst.vv[(size_t)d * R + tid];
         __syncthreads();
@@ -530,21 +643,20 @@ __global__ __launch_bounds__(NT) void fold_block_kernel(int mode, BatchView dst,
     if (__syncthreads_or(err != 0) && tid == 0) atomicOr(wk.status, kErrActorRange);
 }
 
-constexpr int kFoldWaves = 2;
 constexpr int kFoldNT = 256;
 constexpr int kFoldIPT = 4;
 
 hipError_t launch_fold(int mode, const BatchView& dst, const SrcView& sb, const OutView& out, const Scratch& scr,
                        const Work& wk, uint32_t block_grid, hipStream_t stream) {
     if (dst.n_docs == 0) return hipSuccess;
-    uint32_t grid = (dst.n_docs + kFoldWaves - 1) / kFoldWaves;
-    if (grid > (1u << 20)) grid = 1u << 20;
+    const uint32_t per_block = kFoldWaves * kFoldK;
+    const uint32_t grid = (dst.n_docs + per_block - 1) / per_block;
     if (mode == CRDT_FOLD_DELTA)
-        hipLaunchKernelGGL((fold_sort_kernel<kFoldWaves, true>), dim3(grid), dim3(kFoldWaves * 64), 0, stream, dst, sb,
+        hipLaunchKernelGGL((fold_pipe_kernel<kFoldK, true>), dim3(grid), dim3(kFoldWaves * 64), 0, stream, dst, sb,
                            out, wk);
     else
-        hipLaunchKernelGGL((fold_sort_kernel<kFoldWaves, false>), dim3(grid), dim3(kFoldWaves * 64), 0, stream, dst,
-                           sb, out, wk);
+        hipLaunchKernelGGL((fold_pipe_kernel<kFoldK, false>), dim3(grid), dim3(kFoldWaves * 64), 0, stream, dst, sb,
+                           out, wk);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL((fold_block_kernel<kFoldNT, kFoldIPT>), dim3(block_grid), dim3(kFoldNT), 0, stream, mode, dst,

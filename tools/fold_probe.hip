@@ -1,0 +1,97 @@
+// Diagnostic probe (GPU box only, never part of the product): builds the
+// fold kernels with CRDT_STAMPS and reports where a wave's cycles go, phase by
+// phase, for the config-3 (delta) and config-5 (replicas) workloads.  The
+// stamped build is slower than the real kernel; read the SHARES, not the
+// time (cdna_hip_programming.md s7, "In-kernel stamps").
+//
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -DCRDT_STAMPS tools/fold_probe.hip -o tools/fold_probe
+//   tools/fold_probe [config 3|5] [docs]
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#include "../go-crdt-playground_amd/csrc/fold.hip"
+#include "../go-crdt-playground_amd/csrc/gen.hip"
+#include "../go-crdt-playground_amd/csrc/reduce.hip"
+
+using namespace crdt;
+
+#define CK(x)                                                                        \
+    do {                                                                             \
+        hipError_t e_ = (x);                                                         \
+        if (e_ != hipSuccess) {                                                      \
+            fprintf(stderr, "%s:%d %s: %s\n", __FILE__, __LINE__, #x, hipGetErrorString(e_)); \
+            exit(2);                                                                 \
+        }                                                                            \
+    } while (0)
+
+template <typename T>
+T* dalloc(size_t n) {
+    void* p = nullptr;
+    CK(hipMalloc(&p, (n ? n : 1) * sizeof(T)));
+    return (T*)p;
+}
+
+OutView make_out(uint32_t n, uint32_t R, size_t slots) {
+    return OutView{dalloc<uint32_t>(n + 1), dalloc<uint32_t>(n), dalloc<uint64_t>(slots),
+                   dalloc<uint32_t>(slots), dalloc<uint64_t>(slots), dalloc<uint64_t>((size_t)n * R)};
+}
+
+int main(int argc, char** argv) {
+    const int config = argc > 1 ? atoi(argv[1]) : 3;
+    const uint32_t n = argc > 2 ? (uint32_t)atoi(argv[2]) : (config == 5 ? 4000000u : 1048576u);
+    const uint32_t R = config == 5 ? 8 : 16, M = config == 5 ? 7 : 10;
+    const uint32_t E = config == 5 ? 16 : 8, X = config == 5 ? 0 : 2, nd = config == 5 ? 16 : 64;
+    OutView D = make_out(n, R, (size_t)n * nd);
+    const size_t ns = (size_t)n * M;
+    SrcOutView S{dalloc<uint32_t>(n + 1),   dalloc<uint32_t>(ns),          dalloc<uint64_t>(ns * R),
+                 dalloc<uint32_t>(ns + 1),  dalloc<uint64_t>(ns * E),      dalloc<uint32_t>(ns * E),
+                 dalloc<uint64_t>(ns * E),  dalloc<uint32_t>(ns + 1),      dalloc<uint64_t>(ns * X + 1),
+                 dalloc<uint32_t>(ns * X + 1), dalloc<uint64_t>(ns * X + 1)};
+    if (config == 5)
+        CK(launch_gen_replicas(0x5EED, n, M + 1, E, D, S, 0));
+    else
+        CK(launch_gen_delta(0x5EED, n, R, M, D, S, 0));
+    const size_t oslots = (size_t)n * nd + ns * E;
+    OutView O = make_out(n, R, oslots);
+    uint32_t* ws = dalloc<uint32_t>(64);
+    CK(hipMemset(ws, 0, 64 * 4));
+    Work wk{ws + 16, ws, ws + 1, dalloc<uint32_t>(n), ws + 8};
+    Scratch scr{dalloc<uint64_t>(oslots), dalloc<uint32_t>(oslots), dalloc<uint64_t>(oslots), oslots};
+    BatchView dv{n, R, D.offsets, D.counts, D.keys, D.actors, D.counters, D.vv};
+    SrcView sv{n, R, S.doc_srcs, S.src_actor, S.vv, S.entry_off, S.keys, S.actors, S.counters,
+               X ? S.tomb_off : nullptr, S.tkeys, S.tactors, S.tcounters};
+    const int mode = config == 5 ? CRDT_FOLD_AWSET : CRDT_FOLD_DELTA;
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    const int reps = 5;
+    unsigned long long zero[16] = {0};
+    for (int r = 0; r < reps + 1; ++r) {
+        if (r == 1) {
+            CK(hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), zero, sizeof(zero)));
+            CK(hipEventRecord(e0, 0));
+        }
+        CK(launch_reset_work(ws, 0));
+        CK(launch_fold(mode, dv, sv, O, scr, wk, 512, 0));
+    }
+    CK(hipEventRecord(e1, 0));
+    CK(hipDeviceSynchronize());
+    float ms = 0;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    unsigned long long st[16];
+    CK(hipMemcpyFromSymbol(st, HIP_SYMBOL(g_stamps), sizeof(st)));
+    uint32_t status = 0;
+    CK(hipMemcpy(&status, ws + 16, 4, hipMemcpyDeviceToHost));
+    const char* names[16] = {"stage", "prefetch", "schedule", "classify", "noop+keep", "sort-group", "walk+write",
+                             "", "", "", "", "", "", "", "", "doc-loop"};
+    double tot = 0;
+    for (int i = 0; i < 16; ++i) tot += (double)st[i];
+    printf("config %d: %u docs, %.3f ms per stamped launch, status %u\n", config, n, ms / reps, status);
+    printf("wave-cycles per doc (all waves): %.0f\n", tot / reps / n);
+    for (int i = 0; i < 16; ++i)
+        if (st[i]) printf("  %-14s %6.1f%%  %8.0f cyc/doc\n", names[i], 100.0 * st[i] / tot, (double)st[i] / reps / n);
+    return 0;
+}

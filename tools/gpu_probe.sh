@@ -1,0 +1,8 @@
+#!/bin/bash
+# Stamped fold probe (tools/fold_probe.hip, built on the CPU side beforehand).
+set -u
+cd "$(dirname "$0")/.."
+source tools/gpu_step.sh
+TAILN=20
+step probe_c3 120 tools/fold_probe 3
+step probe_c5 120 tools/fold_probe 5
