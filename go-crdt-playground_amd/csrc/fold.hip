@@ -62,8 +62,7 @@ struct FoldSmem {
     uint32_t ta[NCAP];        // tuple actors
     uint32_t soff[MCAP + 1];  // source entry ranges, relative to the first source
     uint32_t sact[MCAP];      // source actors (AWSetDelta.Actor)
-    uint16_t stag[NCAP];      // kept tuples' tags, then the sorted tags
-    uint16_t seg[NCAP + 1];   // first sorted position of each distinct key
+    uint16_t stag[NCAP];      // kept tuples' tags
     uint8_t anye[MCAP];       // step j has a changed entry
     uint8_t anyt[MCAP];       // step j has an effective tombstone
 };
@@ -73,11 +72,32 @@ struct FoldSmem {
 // sort order (key, tag) puts a key's tuples in replay order.
 constexpr uint32_t kPadTag = 0xFFFFu;
 
-// Sort the Kc kept (key, tag) pairs of m.tk / m.stag, then record the groups:
-// m.stag = sorted tags, m.seg[s] = first sorted position of distinct key s,
-// m.tk[s] = that key.  Returns the number of distinct keys.
-template <int EPL>
-__device__ __forceinline__ uint32_t sort_group(FoldSmem& m, uint32_t Kc, uint32_t lane, uint64_t lt) {
+// A document's survivors, at most 4 per lane, in key order: element q of this
+// lane goes to output position off[q] (kOOB: nothing to write).
+struct Emit {
+    uint64_t k[4], c[4];
+    uint32_t a[4], off[4];
+};
+
+// Resolve every key of the document at once, element-parallel.  After the sort
+// a key's kept tuples are consecutive, in replay order (document entry, then by
+// step, an entry before its step's tombstone).  Each tuple acts on the key's
+// presence as a constant or the identity:
+//   document entry                     present (dot := its own)
+//   entry of a full step     (awset.go:122-143) present if the clock before the
+//                            step lacks it, else unchanged (dot := its own)
+//   changed entry, delta step (awset-delta_test.go:126-147) present (dot := own)
+//   effective tombstone      (:149-164) absent if the clock before the step
+//                            lacks it, else unchanged (dot unchanged)
+// and between a tuple and the key's next one (or the end), every full step
+// whose source clock has seen the current dot removes it (awset.go:147-158).
+// The current dot is the last entry's, whatever the presence, so it is one
+// segmented scan; with the gap folded in, each tuple is again constant or
+// identity, and the final presence is the last constant: a second scan.
+template <int EPL, bool DELTA>
+__device__ __forceinline__ uint32_t sort_resolve(const FoldSmem& m, uint32_t Kc, uint32_t ms, uint32_t R,
+                                                 uint64_t full_mask, uint32_t lane, uint64_t lt, Emit& e,
+                                                 uint32_t& err STAMP_PARAM) {
     uint64_t k[EPL];
     uint32_t t[EPL];
 #pragma unroll
@@ -86,108 +106,117 @@ __device__ __forceinline__ uint32_t sort_group(FoldSmem& m, uint32_t Kc, uint32_
         k[q] = i < Kc ? m.tk[i] : ~0ull;
         t[q] = i < Kc ? (uint32_t)m.stag[i] : kPadTag;
     }
-    wave_sync();
     wave_sort_pairs<EPL>(k, t, Kc, lane);
-    bool head[EPL];
-    uint32_t pre = 0;
-    const uint32_t U = segment_heads<EPL>(k, t, kPadTag, lane, lt, head, pre);
+    STAMP(7)
+    // the element after each one (the next lane's first for the last slot)
+    const uint64_t k_nl = from_next_lane64(~0ull, k[0]);
+    const uint32_t t_nl = from_next_lane(kPadTag, t[0]);
+    const uint64_t k_pl = (uint64_t)__shfl_up((unsigned long long)k[EPL - 1], 1);
+
+    // per element: flags, the current dot (da, dc) and the gap's full steps g
+    enum : uint32_t {
+        F_PRES = 1u, F_ABS = 2u,  // presence code of the tuple alone (neither: unchanged)
+        F_HEAD = 4u, F_TAIL = 8u, F_ENT = 16u, F_TOMB = 32u, F_SRC = 64u, F_FULL = 128u,
+        F_AR = 256u,   // the tuple's actor == R (HasDot panics if the reference evaluates it)
+        F_GAP = 512u,  // a full step lies between this tuple and the key's next one
+        F_G = 1024u    // a gap step's source clock has seen the current dot
+    };
+    uint32_t fl[EPL], da[EPL], xd[EPL], dinc[EPL], dexc[EPL];
+    uint64_t dc[EPL], g[EPL];
 #pragma unroll
     for (int q = 0; q < EPL; ++q) {
         const uint32_t i = lane * EPL + q;
-        if (i < Kc) m.stag[i] = (uint16_t)t[q];
-        if (head[q]) {
-            m.seg[pre] = (uint16_t)i;
-            m.tk[pre] = k[q];
-            ++pre;
+        const bool valid = t[q] != kPadTag;
+        const uint32_t hi = t[q] >> 8, ti = valid ? t[q] & 0xFFu : 0u;
+        const bool src = valid && hi != 0, tomb = valid && (hi & 1u);
+        const uint32_t j = src ? ((hi >> 1) - 1u) & 63u : 0u;
+        const bool head = !valid || i == 0 || k[q] != (q == 0 ? k_pl : k[q - 1]);
+        const uint64_t kn = q + 1 < EPL ? k[q + 1] : k_nl;
+        const uint32_t tn = q + 1 < EPL ? t[q + 1] : t_nl;
+        const bool tl = valid && (tn == kPadTag || kn != k[q]);
+        const uint32_t jn = tl ? ms : ((tn >> 9) - 1u);
+        const uint32_t j0 = src ? j + 1u : 0u;
+        g[q] = valid ? (full_mask & low_mask(jn) & ~low_mask(j0)) : 0ull;
+        da[q] = m.ta[ti];
+        dc[q] = m.tc[ti];
+        const uint32_t ar = da[q] < R ? da[q] : 0u;
+        const bool hv = src && da[q] < R && m.vs[j * R + ar] >= dc[q];  // clock before the step has it
+        const bool full = src && ((full_mask >> j) & 1ull);
+        uint32_t f = F_PRES;
+        if (tomb) f = hv ? 0u : F_ABS;
+        else if (full) f = hv ? 0u : F_PRES;
+        f |= (head ? F_HEAD : 0u) | (tl ? F_TAIL : 0u) | ((valid && !tomb) ? F_ENT : 0u) | (tomb ? F_TOMB : 0u) |
+             (src ? F_SRC : 0u) | (full ? F_FULL : 0u) | (da[q] == R ? F_AR : 0u) | (g[q] ? F_GAP : 0u);
+        fl[q] = f;
+        xd[q] = (head || (f & F_ENT)) ? (0x80000000u | ((f & F_ENT) ? 0x100u | ti : 0u)) : 0u;
+    }
+    STAMP(8)
+    scan_last_marked<EPL>(xd, dinc, dexc);
+    // current dot: the key's last entry at or before the tuple
+#pragma unroll
+    for (int q = 0; q < EPL; ++q) {
+        if (!(fl[q] & F_ENT)) {
+            const bool has = dinc[q] & 0x100u;
+            const uint32_t src = dinc[q] & 0xFFu;
+            da[q] = has ? m.ta[src] : 0u;
+            dc[q] = has ? m.tc[src] : 0ull;
         }
+        if (da[q] >= R) g[q] = 0;  // never seen: no gap step removes it
     }
-    if (lane == 0) m.seg[U] = (uint16_t)Kc;
-    wave_sync();
-    return U;
-}
-
-// (no bool members: a struct copy with padding bytes goes through scratch)
-struct KeyFate {
-    uint64_t key, c;
-    uint32_t a, emit;
-};
-
-// Replay the events of distinct key s (< U) in step order.
-template <bool DELTA>
-__device__ __forceinline__ KeyFate walk_key(const FoldSmem& m, uint32_t s, uint32_t U, uint32_t R,
-                                            uint64_t full_mask, uint32_t& err) {
-    const bool act = s < U;
-    uint32_t p = act ? m.seg[s] : 0u;
-    const uint32_t p1 = act ? m.seg[s + 1] : 0u;
-    KeyFate f;
-    f.key = m.tk[act ? s : 0u];
-    uint32_t tg = act ? m.stag[p] : kPadTag;
-    bool pres = false;
-    uint32_t a = 0;
-    uint64_t c = 0;
-    if ((tg >> 8) == 0) {  // the document's own entry
-        pres = true;
-        a = m.ta[tg & 0xFF];
-        c = m.tc[tg & 0xFF];
-        ++p;
-        tg = p < p1 ? m.stag[p] : kPadTag;
-    }
-    uint32_t jn = 0;  // first step not yet replayed
+    // the gaps' full steps, one step per element per round, until one has seen the dot
     for (;;) {
-        // next event: this key's next tuple, or (while present) the next full step
-        const uint32_t ts = tg == kPadTag ? 64u : ((tg >> 9) - 1u);
-        const uint64_t fm = pres && jn < 64 ? (full_mask & (~0ull << jn)) : 0ull;
-        const uint32_t nf = fm ? (uint32_t)__builtin_ctzll(fm) : 64u;
-        const uint32_t je = ts < nf ? ts : nf;
-        const bool go = act && je < 64;
-        if (!ballot(go)) break;
-        if (go) {
-            const bool full = (full_mask >> je) & 1ull;
-            bool is_e = false, is_t = false;
-            uint32_t ea = 0, xa = 0;
-            uint64_t ec = 0, xc = 0;
-            if (ts == je && !((tg >> 8) & 1u)) {
-                is_e = true;
-                ea = m.ta[tg & 0xFF];
-                ec = m.tc[tg & 0xFF];
-                ++p;
-                tg = p < p1 ? m.stag[p] : kPadTag;
-            }
-            if (DELTA && tg != kPadTag && ((tg >> 9) - 1u) == je) {  // tombstone of the same step
-                is_t = true;
-                xa = m.ta[tg & 0xFF];
-                xc = m.tc[tg & 0xFF];
-                ++p;
-                tg = p < p1 ? m.stag[p] : kPadTag;
-            }
-            if (full) {
-                if (is_e) {
-                    // awset.go:122-143: common key -> src dot; src-only -> added iff dst clock lacks it
-                    if (pres || !has_dot_bf(m.vs + je * R, R, ea, ec, true, err)) {
-                        pres = true;
-                        a = ea;
-                        c = ec;
-                    }
-                } else if (pres && has_dot_bf(m.svv + je * R, R, a, c, true, err)) {
-                    pres = false;  // awset.go:150-155: src saw it and dropped it
-                }
-            } else {
-                if (is_e) {  // changed entry: deltaMerge phase 1 (awset-delta_test.go:126-147)
-                    pres = true;
-                    a = ea;
-                    c = ec;
-                }
-                // phase 2 (:149-164): an effective tombstone removes a present
-                // key unless the clock before this step already holds its dot
-                if (is_t && pres && !has_dot_bf(m.vs + je * R, R, xa, xc, true, err)) pres = false;
-            }
-            jn = je + 1;
+        bool any = false;
+#pragma unroll
+        for (int q = 0; q < EPL; ++q) any |= g[q] != 0;
+        if (!ballot(any)) break;
+#pragma unroll
+        for (int q = 0; q < EPL; ++q) {
+            const uint32_t j = g[q] ? (uint32_t)__builtin_ctzll(g[q]) : 0u;
+            const bool seen = g[q] && m.svv[j * R + (da[q] < R ? da[q] : 0u)] >= dc[q];
+            fl[q] |= seen ? F_G : 0u;
+            g[q] = seen ? 0ull : (g[q] & (g[q] - 1ull));
         }
     }
-    f.emit = (act && pres) ? 1u : 0u;
-    f.a = a;
-    f.c = c;
-    return f;
+    STAMP(9)
+    uint32_t xp[EPL], pinc[EPL], pexc[EPL];
+#pragma unroll
+    for (int q = 0; q < EPL; ++q) {
+        const uint32_t h = (fl[q] & F_G) ? F_ABS : (fl[q] & (F_PRES | F_ABS));
+        xp[q] = ((fl[q] & F_HEAD) || h) ? (0x80000000u | (h == F_PRES ? 1u : 0u)) : 0u;
+    }
+    scan_last_marked<EPL>(xp, pinc, pexc);
+    uint32_t ne = 0, perr = 0;
+    bool em[EPL];
+#pragma unroll
+    for (int q = 0; q < EPL; ++q) {
+        const uint32_t f = fl[q];
+        const bool before = !(f & F_HEAD) && (pexc[q] & 1u);  // present before the tuple
+        const bool after = (f & F_PRES) || (!(f & (F_PRES | F_ABS)) && before);
+        if ((f & F_FULL) && (f & F_ENT) && !before && (f & F_AR)) perr = 1;  // awset.go:129 HasDot
+        if (DELTA && (f & F_TOMB) && before && (f & F_AR)) perr = 1;         // delta phase 2 HasDot
+        if (after && da[q] == R && (f & F_GAP)) perr = 1;                    // awset.go:151 HasDot
+        em[q] = (f & F_TAIL) && (pinc[q] & 1u);
+        ne += em[q] ? 1u : 0u;
+    }
+    if (perr) err |= kErrActorRange;
+    uint32_t pre = 0;
+    const uint32_t tot = lane_prefix_small(ne, lt, pre);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        if (q < EPL) {
+            e.k[q] = k[q];
+            e.a[q] = da[q];
+            e.c[q] = dc[q];
+            e.off[q] = em[q] ? pre : kOOB;
+            pre += em[q] ? 1u : 0u;
+        } else {
+            e.k[q] = 0;
+            e.a[q] = 0;
+            e.c[q] = 0;
+            e.off[q] = kOOB;
+        }
+    }
+    return tot;
 }
 
 // One document's inputs, loaded a document ahead.
@@ -205,7 +234,7 @@ constexpr int kFoldK = 32;     // consecutive documents per wavefront
 constexpr int kFoldStores = 4 * 3 + 2;  // stores of one document's write-out (walk rounds x 3 + count + VV)
 
 template <int K, bool DELTA>
-__global__ __launch_bounds__(kFoldWaves * 64) void fold_pipe_kernel(BatchView dst, SrcView sb, OutView out, Work wk) {
+__global__ __launch_bounds__(kFoldWaves * 64) __attribute__((amdgpu_waves_per_eu(3))) void fold_pipe_kernel(BatchView dst, SrcView sb, OutView out, Work wk) {
     using Smem = FoldSmem;
     __shared__ Smem smem[kFoldWaves];
     const uint32_t lane = threadIdx.x & 63;
@@ -358,7 +387,8 @@ __global__ __launch_bounds__(kFoldWaves * 64) void fold_pipe_kernel(BatchView ds
 
         // ---- fold document k
         uint64_t vfin = 0, full_mask = 0;
-        uint32_t U = 0;
+        uint32_t U = 0;  // survivors
+        Emit em;
         if (!cur.big) {
             const uint32_t n = cur.n, E = cur.E, N = cur.N, ms = cur.ms;
             // schedule: U_j, one lane per actor
@@ -524,28 +554,30 @@ __global__ __launch_bounds__(kFoldWaves * 64) void fold_pipe_kernel(BatchView ds
             }
             wave_sync();
             STAMP(4)
-            U = Kc <= 64 ? sort_group<1>(m, Kc, lane, lt)
-                         : (Kc <= 128 ? sort_group<2>(m, Kc, lane, lt) : sort_group<4>(m, Kc, lane, lt));
+            U = Kc <= 64    ? sort_resolve<1, DELTA>(m, Kc, ms, R, full_mask, lane, lt, em, err STAMP_ARGS)
+                : Kc <= 128 ? sort_resolve<2, DELTA>(m, Kc, ms, R, full_mask, lane, lt, em, err STAMP_ARGS)
+                            : sort_resolve<4, DELTA>(m, Kc, ms, R, full_mask, lane, lt, em, err STAMP_ARGS);
             STAMP(5)
         }
-        // ---- walk the keys and write the survivors (every store unconditional)
+        // ---- write the survivors (every store unconditional)
         const uint32_t obase = cur.doff + cur.e0;
         const uint32_t capo = cur.big ? 0u : min(cur.slots + cur.E, (uint32_t)Smem::NCAP);
         const rsrc_t ok = make_rsrc(out.keys + obase, capo * 8u), oa = make_rsrc(out.actors + obase, capo * 4u),
                      oc = make_rsrc(out.counters + obase, capo * 8u);
-        uint32_t carry = 0;
+        if (cur.big) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            KeyFate f{0ull, 0ull, 0u, 0u};
-            if (!cur.big && (uint32_t)r * 64u < U) f = walk_key<DELTA>(m, r * 64u + lane, U, R, full_mask, err);
-            const uint64_t em = ballot(f.emit);
-            const uint32_t pos = carry + popc(em & lt);
-            carry += popc(em);
-            const uint32_t o8 = f.emit ? pos * 8u : kOOB, o4 = f.emit ? pos * 4u : kOOB;
-            st64<kAuxNT>(f.key, ok, o8);
-            st32<kAuxNT>(f.a, oa, o4);
-            st64<kAuxNT>(f.c, oc, o8);
+            for (int q = 0; q < 4; ++q) em.off[q] = kOOB;
+            U = 0;
         }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint32_t o = em.off[q];
+            const uint32_t o8 = o == kOOB ? kOOB : o * 8u, o4 = o == kOOB ? kOOB : o * 4u;
+            st64<kAuxNT>(em.k[q], ok, o8);
+            st32<kAuxNT>(em.a[q], oa, o4);
+            st64<kAuxNT>(em.c[q], oc, o8);
+        }
+        const uint32_t carry = U;
         st32(carry, make_rsrc(out.counts + cur.d, cur.big ? 0u : 4u), lane == 0 ? 0u : kOOB);
         st64(vfin, make_rsrc(out.vv + (size_t)cur.d * R, cur.big ? 0u : R * 8u), lane * 8u);
         wave_sync();

@@ -111,6 +111,32 @@ __device__ __forceinline__ void bitonic_step_packed(uint64_t (&v)[EPL], uint32_t
     if constexpr (JJ > 1) bitonic_step_packed<EPL, KK, JJ / 2>(v, lane);
 }
 
+// The network over packed 32-bit values ((key offset) << 16 | tag): one DPP
+// exchange, one compare and one select per element and stage.
+template <int EPL, int KK, int JJ>
+__device__ __forceinline__ void bitonic_step32(uint32_t (&v)[EPL], uint32_t lane) {
+    if constexpr (JJ >= EPL) {
+        constexpr int LM = JJ / EPL;
+#pragma unroll
+        for (int q = 0; q < EPL; ++q) {
+            const uint32_t pv = lane_xor<LM>(v[q], lane);
+            const bool take = (pv < v[q]) == keeps_min<EPL, KK, JJ>(lane, q);
+            v[q] = take ? pv : v[q];
+        }
+    } else {
+#pragma unroll
+        for (int q = 0; q < EPL; ++q) {
+            if (q & JJ) continue;
+            const int r = q | JJ;
+            const bool asc = ((lane * EPL + q) & KK) == 0;
+            const uint32_t lo = min(v[q], v[r]), hi = max(v[q], v[r]);
+            v[q] = asc ? lo : hi;
+            v[r] = asc ? hi : lo;
+        }
+    }
+    if constexpr (JJ > 1) bitonic_step32<EPL, KK, JJ / 2>(v, lane);
+}
+
 // Sort the wavefront's EPL*64 pairs ascending by (key, tag).
 template <int EPL, int KK = 2>
 __device__ __forceinline__ void wave_bitonic(uint64_t (&k)[EPL], uint32_t (&t)[EPL], uint32_t lane) {
@@ -119,53 +145,56 @@ __device__ __forceinline__ void wave_bitonic(uint64_t (&k)[EPL], uint32_t (&t)[E
 }
 
 template <int EPL, int KK = 2>
+__device__ __forceinline__ void wave_bitonic32(uint32_t (&v)[EPL], uint32_t lane) {
+    bitonic_step32<EPL, KK, KK / 2>(v, lane);
+    if constexpr (KK < EPL * 64) wave_bitonic32<EPL, KK * 2>(v, lane);
+}
+
+template <int EPL, int KK = 2>
 __device__ __forceinline__ void wave_bitonic_packed(uint64_t (&v)[EPL], uint32_t lane) {
     bitonic_step_packed<EPL, KK, KK / 2>(v, lane);
     if constexpr (KK < EPL * 64) wave_bitonic_packed<EPL, KK * 2>(v, lane);
 }
 
-// 64-bit min / max over the wavefront (every lane gets the result).
-__device__ __forceinline__ uint64_t wave_min64(uint64_t x) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        const uint64_t y = (uint64_t)__shfl_xor((unsigned long long)x, o);
-        x = y < x ? y : x;
-    }
-    return x;
-}
-__device__ __forceinline__ uint64_t wave_max64(uint64_t x) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        const uint64_t y = (uint64_t)__shfl_xor((unsigned long long)x, o);
-        x = y > x ? y : x;
-    }
-    return x;
-}
-
 // Sort n <= EPL*64 (key, tag) pairs (tags < 0xFFFF, unique per key; slots past
-// n are padding): packed into one 64-bit value when the keys span less than
-// 2^48, the general 80-bit comparison otherwise.  Returns with the pairs in
-// element order and pads (key ~0, tag 0xFFFF) at the end.
+// n are padding).  Keys are taken relative to the first pair's key b: when
+// every key lies in [b - 2^15, b + 2^15) the pair packs into 32 bits (offset
+// << 16 | tag), when within [b - 2^47, b + 2^47) into 64 bits, both
+// order-preserving; otherwise the 80-bit comparison runs.  Returns with the
+// pairs in element order and pads (key ~0, tag 0xFFFF) last.
 template <int EPL>
 __device__ __forceinline__ void wave_sort_pairs(uint64_t (&k)[EPL], uint32_t (&t)[EPL], uint32_t n, uint32_t lane) {
-    uint64_t lo = ~0ull, hi = 0;
+    const uint64_t b = readlane64(k[0], 0);
+    bool o16 = false, o48 = false;
 #pragma unroll
     for (int q = 0; q < EPL; ++q) {
-        const bool v = lane * EPL + q < n;
-        lo = v && k[q] < lo ? k[q] : lo;
-        hi = v && k[q] > hi ? k[q] : hi;
+        const bool valid = lane * EPL + q < n;
+        const uint64_t d = k[q] - b;
+        o16 |= valid && d + 0x8000ull >= 0x10000ull;
+        o48 |= valid && d + (1ull << 47) >= (1ull << 48);
     }
-    const uint64_t kmin = wave_min64(lo), kmax = wave_max64(hi);
-    if (n == 0 || kmax - kmin < (1ull << 48)) {
+    if (!ballot(o16)) {
+        uint32_t v[EPL];
+#pragma unroll
+        for (int q = 0; q < EPL; ++q)
+            v[q] = lane * EPL + q < n ? ((uint32_t)(k[q] - b + 0x8000ull) << 16) | (t[q] & 0xFFFFu) : ~0u;
+        wave_bitonic32<EPL>(v, lane);
+#pragma unroll
+        for (int q = 0; q < EPL; ++q) {
+            const bool pad = v[q] == ~0u;
+            k[q] = pad ? ~0ull : b - 0x8000ull + (v[q] >> 16);
+            t[q] = pad ? 0xFFFFu : (v[q] & 0xFFFFu);
+        }
+    } else if (!ballot(o48)) {
         uint64_t v[EPL];
 #pragma unroll
         for (int q = 0; q < EPL; ++q)
-            v[q] = lane * EPL + q < n ? ((k[q] - kmin) << 16) | (uint64_t)(t[q] & 0xFFFFu) : ~0ull;
+            v[q] = lane * EPL + q < n ? ((k[q] - b + (1ull << 47)) << 16) | (uint64_t)(t[q] & 0xFFFFu) : ~0ull;
         wave_bitonic_packed<EPL>(v, lane);
 #pragma unroll
         for (int q = 0; q < EPL; ++q) {
             const bool pad = v[q] == ~0ull;
-            k[q] = pad ? ~0ull : (v[q] >> 16) + kmin;
+            k[q] = pad ? ~0ull : b - (1ull << 47) + (v[q] >> 16);
             t[q] = pad ? 0xFFFFu : (uint32_t)(v[q] & 0xFFFFu);
         }
     } else {
@@ -173,32 +202,59 @@ __device__ __forceinline__ void wave_sort_pairs(uint64_t (&k)[EPL], uint32_t (&t
     }
 }
 
-// Heads of the sorted pairs: the first pair of each distinct key (pads, tag ==
-// pad, are never heads).  head[q] per element; pre = number of heads before
-// this lane's elements (bit-sliced ballots of the per-lane counts, <= 4).
-// Returns the number of heads.
+// ---- DPP lane shifts and the segmented "last marked value" scan (gfx9 DPP:
+// row_shr, row_bcast, wave_shl/shr; lanes with no source take `old`).
+template <int CTRL, int ROWS = 0xF>
+__device__ __forceinline__ uint32_t dpp(uint32_t old, uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)v, CTRL, ROWS, 0xF, false);
+}
+// value of lane + 1 (lane 63: old)
+__device__ __forceinline__ uint32_t from_next_lane(uint32_t old, uint32_t v) { return dpp<0x130>(old, v); }
+__device__ __forceinline__ uint64_t from_next_lane64(uint64_t old, uint64_t v) {
+    return (uint64_t)from_next_lane((uint32_t)old, (uint32_t)v) |
+           ((uint64_t)from_next_lane((uint32_t)(old >> 32), (uint32_t)(v >> 32)) << 32);
+}
+
+// Elements carry x = 0 (unmarked) or 0x80000000 | value (marked).  incl[q] =
+// the x of the last marked element at or before element q (0 if none);
+// excl[q] = the same strictly before q.  Segment heads are marked by the
+// caller, so nothing crosses a segment boundary.  Lane-local pass, then a
+// Hillis-Steele pass over lanes with DPP (no LDS).
 template <int EPL>
-__device__ __forceinline__ uint32_t segment_heads(const uint64_t (&k)[EPL], const uint32_t (&t)[EPL], uint32_t pad,
-                                                  uint32_t lane, uint64_t lt, bool (&head)[EPL], uint32_t& pre) {
-    static_assert(EPL <= 4, "segment_heads: at most 4 elements per lane");
-    const uint64_t prev = (uint64_t)__shfl_up((unsigned long long)k[EPL - 1], 1);
-    uint32_t hc = 0;
+__device__ __forceinline__ void scan_last_marked(const uint32_t (&x)[EPL], uint32_t (&incl)[EPL], uint32_t (&excl)[EPL]) {
+    uint32_t loc[EPL], acc = 0;
 #pragma unroll
     for (int q = 0; q < EPL; ++q) {
-        const uint32_t i = lane * EPL + q;
-        const uint64_t pk = q == 0 ? prev : k[q - 1];
-        head[q] = t[q] != pad && (i == 0 || k[q] != pk);
-        hc += head[q] ? 1u : 0u;
+        acc = (x[q] >> 31) ? x[q] : acc;
+        loc[q] = acc;
     }
-    uint32_t U = 0;
+    uint32_t s = acc, y;
+    y = dpp<0x111>(0u, s); s = (s >> 31) ? s : y;        // row_shr:1
+    y = dpp<0x112>(0u, s); s = (s >> 31) ? s : y;        // row_shr:2
+    y = dpp<0x114>(0u, s); s = (s >> 31) ? s : y;        // row_shr:4
+    y = dpp<0x118>(0u, s); s = (s >> 31) ? s : y;        // row_shr:8
+    y = dpp<0x142, 0xA>(0u, s); s = (s >> 31) ? s : y;   // row_bcast:15 -> rows 1, 3
+    y = dpp<0x143, 0xC>(0u, s); s = (s >> 31) ? s : y;   // row_bcast:31 -> rows 2, 3
+    uint32_t prev = dpp<0x138>(0u, s);                    // wave_shr:1: lanes before this one
+#pragma unroll
+    for (int q = 0; q < EPL; ++q) {
+        excl[q] = prev;
+        incl[q] = (loc[q] >> 31) ? loc[q] : prev;
+        prev = incl[q];
+    }
+}
+
+// Exclusive prefix count of per-lane counts c (<= 7) in lane order; returns the total.
+__device__ __forceinline__ uint32_t lane_prefix_small(uint32_t c, uint64_t lt, uint32_t& pre) {
+    uint32_t tot = 0;
     pre = 0;
 #pragma unroll
     for (int b = 0; b < 3; ++b) {
-        const uint64_t mb = ballot((hc >> b) & 1u);
+        const uint64_t mb = ballot((c >> b) & 1u);
         pre += popc(mb & lt) << b;
-        U += popc(mb) << b;
+        tot += popc(mb) << b;
     }
-    return U;
+    return tot;
 }
 
 }  // namespace crdt

@@ -1,14 +1,17 @@
-"""CPU: the per-key restatement of the ordered fold that fold_sort_kernel
+"""CPU: the per-key restatement of the ordered fold that fold_pipe_kernel
 (go-crdt-playground_amd/csrc/fold.hip) implements, checked against the C oracle
 (step-by-step replay of awset.go:103-161 / awset-delta_test.go:51-166) on
 randomized adversarial documents -- tombstones (effective and re-added),
 no-op delta steps, first contact (Counter(src.Actor) == 0), keys known only to
 sources, actor == len(VV) panics and actor > len(VV).
 
-The model follows the kernel's four phases literally (schedule, keep/tag,
-sort by (key, tag), event walk per key), so a pass here says the
-formulation is the reference's semantics, including which HasDot calls can
-panic; the GPU tests then check the kernel against the same oracle."""
+The model follows the kernel's phases literally (schedule, keep/tag, sort by
+(key, tag), then the element-parallel resolve of fold.hip sort_resolve: a
+segmented scan for the current dot, the gap removals, a segmented scan for the
+presence), and keeps the sequential event walk per key beside it as a second
+restatement, so a pass here says the formulation is the reference's
+semantics, including which HasDot calls can panic; the GPU tests then check
+the kernel against the same oracle."""
 
 import random
 
@@ -17,6 +20,66 @@ import pytest
 from crdtgpu import CRDT_FOLD_AWSET, CRDT_FOLD_DELTA
 from crdtgpu.batch import AWSetBatch, SrcBatch
 from oracle import oracle
+
+
+def resolve_scan(tup, chain, full, Vs, R, delta):
+    """fold.hip sort_resolve over the sorted kept tuples: returns (err, out)."""
+    M = len(chain)
+    n = len(tup)
+    err = False
+    step = [-1 if z[1] == 0 else (z[1] >> 1) - 1 for z in tup]
+    tomb = [z[1] & 1 == 1 for z in tup]
+    ent = [not x for x in tomb]
+    head = [i == 0 or tup[i][0] != tup[i - 1][0] for i in range(n)]
+    tail = [i == n - 1 or tup[i + 1][0] != tup[i][0] for i in range(n)]
+
+    def scan_last(marked, val):
+        """inclusive / exclusive 'last marked value' (None = no mark)."""
+        inc, exc, cur = [], [], None
+        for i in range(n):
+            exc.append(cur)
+            if marked[i]:
+                cur = val[i]
+            inc.append(cur)
+        return inc, exc
+
+    # the clock before the tuple's step has the tuple's dot (source tuples)
+    hv = [step[i] >= 0 and tup[i][2] < R and Vs[step[i]][tup[i][2]] >= tup[i][3] for i in range(n)]
+    f = []  # 1 present, 2 absent, 0 unchanged
+    for i in range(n):
+        if step[i] < 0:
+            f.append(1)
+        elif tomb[i]:
+            f.append(0 if hv[i] else 2)
+        elif full[step[i]]:
+            f.append(0 if hv[i] else 1)
+        else:
+            f.append(1)
+    dinc, _ = scan_last([head[i] or ent[i] for i in range(n)], [i if ent[i] else None for i in range(n)])
+    da = [tup[dinc[i]][2] if dinc[i] is not None else 0 for i in range(n)]
+    dc = [tup[dinc[i]][3] if dinc[i] is not None else 0 for i in range(n)]
+    gaps, G = [], []
+    for i in range(n):
+        jn = M if tail[i] else step[i + 1]
+        g = [j for j in range(step[i] + 1, jn) if full[j]]
+        gaps.append(g)
+        G.append(da[i] < R and any(chain[j][1][da[i]] >= dc[i] for j in g))
+    h = [2 if G[i] else f[i] for i in range(n)]
+    pinc, pexc = scan_last([head[i] or h[i] != 0 for i in range(n)], [h[i] == 1 for i in range(n)])
+    out = []
+    for i in range(n):
+        before = not head[i] and bool(pexc[i])
+        after = f[i] == 1 or (f[i] == 0 and before)
+        a = tup[i][2]
+        if step[i] >= 0 and full[step[i]] and ent[i] and not before and a == R:
+            err = True
+        if delta and tomb[i] and before and a == R:
+            err = True
+        if after and da[i] == R and gaps[i]:
+            err = True
+        if tail[i] and pinc[i]:
+            out.append((tup[i][0], da[i], dc[i]))
+    return err, out
 
 
 def model_fold(mode, ents, vv0, chain):
@@ -73,6 +136,8 @@ def model_fold(mode, ents, vv0, chain):
                     tup.append((k, (j + 1) * 2 + 1, a, c))
     # 3. group by key in replay order
     tup.sort(key=lambda z: (z[0], z[1]))
+    err_scan, out_scan = resolve_scan(tup, chain, full, Vs, R, delta)
+    err_scan |= err  # panics of the schedule are the kernel's classify phase
     segs = {}
     for z in tup:
         segs.setdefault(z[0], []).append(z)
@@ -112,6 +177,9 @@ def model_fold(mode, ents, vv0, chain):
             jn = je + 1
         if pres:
             out.append((key, a, c))
+    assert err_scan == err
+    if not err:
+        assert out_scan == out
     return err, out, V
 
 

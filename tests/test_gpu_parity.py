@@ -218,6 +218,73 @@ def test_fold_block_path_and_overflow(eng, mode):
     assert_same(eng.fold(mode, dst, srcs), want, dst.n_docs, R)
 
 
+@pytest.mark.parametrize("mode", [CRDT_FOLD_AWSET, CRDT_FOLD_DELTA])
+def test_fold_wide_key_spans(eng, mode):
+    """The in-register sort packs (key, tag) into 32 bits when a document's keys
+    lie within 2^15 of its first kept key, into 64 bits within 2^47, and falls
+    back to the 80-bit comparison beyond: every tier, mixed in one batch, and
+    keys at both ends of the u64 range."""
+    rng = random.Random(40 + mode)
+    R = 4
+    delta = mode == CRDT_FOLD_DELTA
+    top = (1 << 64) - 1
+    # per-document monotone key maps: dense, spread beyond 2^16, beyond 2^48, the whole range
+    maps = [lambda k: k, lambda k: (1 << 40) + k * 1021, lambda k: (1 << 62) + k * (1 << 41),
+            lambda k: min(top, k * (top // 199))]
+    dsts, per_doc = [], []
+    for d in range(1200):
+        f = maps[d % len(maps)]
+        mp = lambda es: [(f(k), a, c) for k, a, c in es]
+        e, vv = random_state(rng, R, rng.randint(0, 64), 200, 8)
+        dsts.append((mp(e), vv))
+        chain = []
+        for _ in range(rng.randint(0, 8)):
+            se, svv = random_state(rng, R, rng.randint(0, 10), 200, 8)
+            t = mp(random_state(rng, R, rng.randint(0, 3), 200, 8)[0]) if delta else []
+            chain.append((rng.randrange(R), svv, mp(se), t))
+        per_doc.append(chain)
+    dst, srcs = batch_of(R, dsts), src_batch_of(R, per_doc)
+    rc, want = oracle.fold(mode, dst, srcs)
+    assert rc == 0
+    assert_same(eng.fold(mode, dst, srcs), want, dst.n_docs, R)
+
+
+@pytest.mark.parametrize("mode", [CRDT_FOLD_AWSET, CRDT_FOLD_DELTA])
+def test_fold_panic_parity_per_doc(eng, mode):
+    """actor == len(VV) panics exactly where the reference evaluates HasDot on
+    it (a full step's add check, a tombstone's check, a gap step's removal
+    check, the path select), and actor > len(VV) is "never seen": one
+    document per call, the oracle's verdict against the kernel's."""
+    rng = random.Random(50 + mode)
+    R = 3
+    delta = mode == CRDT_FOLD_DELTA
+    seen_err = seen_ok = 0
+
+    def ah():  # now and then a state whose dots name actors R and R + 1
+        return R + 1 if rng.random() < 0.12 else None
+
+    for _ in range(240):
+        e, vv = random_state(rng, R, rng.randint(0, 12), 24, 6, actor_hi=ah())
+        if rng.random() < 0.3:
+            vv[rng.randrange(R)] = 0
+        chain = []
+        for _ in range(rng.randint(1, 5)):
+            se, svv = random_state(rng, R, rng.randint(0, 8), 24, 6, actor_hi=ah())
+            t = random_state(rng, R, rng.randint(0, 3), 24, 6, actor_hi=ah())[0] if delta else []
+            chain.append((rng.randrange(R + 1) if rng.random() < 0.1 else rng.randrange(R), svv, se, t))
+        dst, srcs = batch_of(R, [(e, vv)]), src_batch_of(R, [chain])
+        rc, want = oracle.fold(mode, dst, srcs)
+        if rc != 0:
+            with pytest.raises(crdtgpu.CrdtError) as ei:
+                eng.fold(mode, dst, srcs)
+            assert ei.value.code == crdtgpu.CRDT_E_ACTOR_RANGE, (e, vv, chain)
+            seen_err += 1
+        else:
+            assert_same(eng.fold(mode, dst, srcs), want, 1, R)
+            seen_ok += 1
+    assert seen_err > 10 and seen_ok > 10
+
+
 def test_delta_fold_noop_and_first_contact(eng):
     R = 2
     # dst has seen actor 1 up to 5: src (actor 1) entries covered, no tombstones -> no-op, VV untouched

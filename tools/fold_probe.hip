@@ -85,8 +85,8 @@ int main(int argc, char** argv) {
     CK(hipMemcpyFromSymbol(st, HIP_SYMBOL(g_stamps), sizeof(st)));
     uint32_t status = 0;
     CK(hipMemcpy(&status, ws + 16, 4, hipMemcpyDeviceToHost));
-    const char* names[16] = {"stage", "prefetch", "schedule", "classify", "noop+keep", "sort-group", "walk+write",
-                             "", "", "", "", "", "", "", "", "doc-loop"};
+    const char* names[16] = {"stage", "prefetch", "schedule", "classify", "noop+keep", "sort-group", "write",
+                             "sort", "elem-flags", "dot-scan+gaps", "", "", "", "", "", "doc-loop"};
     double tot = 0;
     for (int i = 0; i < 16; ++i) tot += (double)st[i];
     printf("config %d: %u docs, %.3f ms per stamped launch, status %u\n", config, n, ms / reps, status);
