@@ -1,24 +1,31 @@
 #!/usr/bin/env python3
 """Benchmark: batched AWSet / AWSetDelta merges on MI355X.
 
-Default workload = BASELINE config 2 (the metric's configuration), per GPU
-(weak scaling): 1,048,576 independent documents x 2 replicas, 64 entries per
-replica state, R = 2, synthetic reachable states generated on the device
-(csrc/gen.hip).  One step = one pass of the hot path over the batch:
-  A <- B and B <- A for every document (2 merges per doc, crdt_awset_join_async),
-  then the per-GPU causal-context summary (elementwise max of the output VVs),
-  all-reduced (max, u64) across GPUs over RCCL when N > 1.
---config 3: delta-state anti-entropy -- 10 ordered AWSetDelta sources folded
-  into each of 1,048,576 docs (R = 16): 10,485,760 merges per step.
---config 4: 16,384 docs with Zipf(1.1)-like sizes up to 2^20 entries, 50%
-  concurrent add/remove conflicts, joined both directions (block path).
---config 5: 12.5M docs per GPU (100M over 8 GPUs) x 8 replicas of 16 entries
-  (R = 8) folded r0 <- r1 <- ... <- r7, plus the global causal context.
-Inputs are resident in HBM before the timed region.  Metric: replica merges/s
-(whole job), with the dominant kernel's achieved algorithmic HBM bandwidth
-against the 8 TB/s roofline and the C oracle timed on the host beside it.
+Headline = BASELINE config 2 (the metric's configuration), per GPU (weak
+scaling): 1,048,576 independent documents x 2 replicas, 64 entries per replica
+state, R = 2, synthetic reachable states generated on the device
+(csrc/gen.hip).  One step = one pass of the hot path over the batch: for every
+document the two merges A <- B and B <- A of one snapshot (one exchange launch,
+crdt_awset_exchange_async), then the per-GPU causal-context summary
+(elementwise max of the output VVs), all-reduced (max, u64) across GPUs over
+RCCL when N > 1.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2|3|4|5]
+The same JSON line carries one "legs" entry per other BASELINE config, each
+timed the same way (warmup, barrier + synchronize, K steps, max over ranks),
+with its own roofline, graph-replay check and CPU baseline:
+  config3: 10 ordered AWSetDelta sources folded into each of 1,048,576 docs (R = 16)
+  config4: 16,384 docs with Zipf(1.1)-like sizes up to 2^20 entries, 50%
+           concurrent add/remove conflicts, both directions (block path)
+  config5: 12.5M docs per GPU (100M over 8 GPUs) x 8 replicas of 16 entries
+           (R = 8) folded r0 <- r1 <- ... <- r7, plus the global causal context
+Inputs are resident in HBM before every timed region.  Metric: replica
+merges/s (whole job); roofline: the dominant kernel's algorithmic HBM bytes
+per launch / its mean launch time (HIP events on its stream) against 8 TB/s;
+cpu_baseline: the hash-map C++ restatement of the reference merge
+(oracle/awset_map.cpp) on every host core, with the 1-core figures and the
+sorted-array C oracle beside it.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2|3|4|5] [--legs 3,4,5|none]
   torchrun --nproc-per-node N bench.py --gpus N ...   (one process per GPU)
 """
 
@@ -52,6 +59,24 @@ def _host_batch(o, n_sample, R):
                       counts=_np_copy(o.counts, n_sample, np.uint32))
 
 
+def _host_srcs(S, n_sample, R, per_doc, E, X):
+    """First n_sample docs' sources of a device SrcBuffers (per_doc sources of E entries / X tombstones each)."""
+    import numpy as np
+
+    from crdtgpu.batch import SrcBatch
+
+    k = n_sample * per_doc
+    u32, u64 = np.uint32, np.uint64
+    if X:
+        tomb = (_np_copy(S.tomb_off, k + 1, u32), _np_copy(S.tkeys, k * X, u64), _np_copy(S.tactors, k * X, u32),
+                _np_copy(S.tcounters, k * X, u64))
+    else:
+        tomb = ()
+    return SrcBatch(R, _np_copy(S.doc_srcs, n_sample + 1, u32), _np_copy(S.src_actor, k, u32),
+                    _np_copy(S.vv, k * R, u64), _np_copy(S.entry_off, k + 1, u32), _np_copy(S.keys, k * E, u64),
+                    _np_copy(S.actors, k * E, u32), _np_copy(S.counters, k * E, u64), *tomb)
+
+
 def _time_cpu(fn, merges_per_call, budget_s):
     merges, t0 = 0, time.perf_counter()
     while True:
@@ -62,15 +87,42 @@ def _time_cpu(fn, merges_per_call, budget_s):
             return merges, el
 
 
+def _cpu_baselines(label, map_bench, sorted_run, sorted_merges, budget_s):
+    """The hash-map restatement on every host core (the reported value), on one
+    core, and the sorted-array C oracle on one core, each for ~budget_s."""
+    from oracle import oracle
+
+    threads = oracle.cpu_threads()
+    m_all, t_all = map_bench(threads, budget_s)
+    m_one, t_one = map_bench(1, budget_s)
+    m_arr, t_arr = _time_cpu(sorted_run, sorted_merges, budget_s)
+    return {
+        "value": m_all / t_all, "unit": "merges/s", "cores": threads, "kind": "port",
+        "sample": "%s; C++ std::unordered_map<std::string,Dot> restatement of the reference merge "
+                  "(oracle/awset_map.cpp; map[string]Dot as awset.go:55-59), %d threads over documents, maps cloned "
+                  "untimed per pass, %d merges in %.1f s timed (no Go toolchain on the box: the Go reference itself "
+                  "cannot run)" % (label, threads, m_all, t_all),
+        "one_core": {"value": m_one / t_one, "unit": "merges/s", "cores": 1, "kind": "port",
+                     "sample": "same restatement, 1 thread, %d merges in %.1f s" % (m_one, t_one)},
+        "sorted_array_one_core": {"value": m_arr / t_arr, "unit": "merges/s", "cores": 1, "kind": "port",
+                                  "sample": "C oracle (oracle/awset_oracle.c, sorted SoA arrays), 1 thread, "
+                                            "%d merges in %.1f s" % (m_arr, t_arr)},
+    }
+
+
+def _outs(*bufs):
+    return [getattr(b, f) for b in bufs for f in ("offsets", "counts", "keys", "actors", "counters", "vv")]
+
+
 class Config2:
-    """Full-state join, both directions (BASELINE configs[1])."""
+    """Full-state join, both directions of one snapshot (BASELINE configs[1])."""
 
     R = 2
+    name = "config2"
     kernel = "join_wave_kernel"
     metric = "replica-merges/sec (AWSet full-state join) + achieved HBM GB/s (% roofline)"
-
-    exchange = True  # both directions from one read (crdt_awset_exchange_async); --separate: two joins
-    graph_ok = True  # hot() is one kernel launch, replayed from a captured HIP graph (validated on MI355X)
+    exchange = True  # both merges from one read (crdt_awset_exchange_async); --separate: two join launches
+    cpu_docs = 65536
 
     def __init__(self, eng, n, seed, dev, stream):
         import torch
@@ -105,6 +157,9 @@ class Config2:
             self.eng.join_async(ca, cb, cab, stream=s)
             self.eng.join_async(cb, ca, cba, stream=s)
 
+    def outputs(self):
+        return _outs(self.oab, self.oba)
+
     def post(self, s):
         """Per-GPU causal-context summary of the outputs; returns the R-vector."""
         eng, n, R = self.eng, self.n, self.R
@@ -117,28 +172,33 @@ class Config2:
         return 1 if self.exchange else 2
 
     def bytes_per_launch(self):
-        """SURVEY 8d per-merge bytes x the merges one launch performs (exchange: 2 per doc)."""
+        """Algorithmic bytes of one launch: the exchange reads both states once and
+        writes both outputs (workloads.exchange_bytes); separate joins: SURVEY 8d
+        per merge.  Also returns the per-merge SURVEY 8d sum, for reference."""
         from crdtgpu import workloads
 
         cA, cB = self.A.counts.cpu().numpy(), self.B.counts.cpu().numpy()
-        b1 = workloads.join_bytes(cA, cB, self.oab.counts.cpu().numpy(), self.R)
-        b2 = workloads.join_bytes(cB, cA, self.oba.counts.cpu().numpy(), self.R)
-        return (b1 + b2) if self.exchange else (b1 + b2) // 2
+        cab, cba = self.oab.counts.cpu().numpy(), self.oba.counts.cpu().numpy()
+        per_merge = workloads.join_bytes(cA, cB, cab, self.R) + workloads.join_bytes(cB, cA, cba, self.R)
+        if self.exchange:
+            return workloads.exchange_bytes(cA, cB, cab, cba, self.R), per_merge
+        return per_merge // 2, per_merge
 
     @property
     def kernel_name(self):
-        return self.kernel + (" (exchange: both directions, one read)" if self.exchange else "")
+        return self.kernel + (" (exchange: both merges of one snapshot, one read)" if self.exchange else "")
 
     def describe(self, world):
-        return {"workload": "config2: %d docs/GPU x 2 replicas x 64 entries, R=2, full-state join both directions "
-                            "(%s) + causal-context allreduce(max,u64)" % (
+        return {"workload": "config2: %d docs/GPU x 2 replicas x 64 entries, R=2, full-state join: the two merges "
+                            "A<-B and B<-A of one snapshot (%s) + causal-context allreduce(max,u64)" % (
                                 self.n, "one exchange launch" if self.exchange else "two join launches"),
                 "docs_per_gpu": self.n, "replicas": 2, "entries_per_replica": 64, "R": self.R,
                 "merges_per_step": self.merges_per_step * world, "parallelism": "doc-sharded x%d" % world}
 
-    def cpu_baseline(self, n_sample, budget_s):
+    def cpu_baseline(self, budget_s):
         from oracle import oracle
 
+        n_sample = min(self.cpu_docs, self.n)
         ha, hb = _host_batch(self.A, n_sample, self.R), _host_batch(self.B, n_sample, self.R)
 
         def run():
@@ -146,11 +206,8 @@ class Config2:
             rc2, _ = oracle.join(hb, ha)
             assert rc1 == 0 and rc2 == 0
 
-        merges, el = _time_cpu(run, 2 * n_sample, budget_s)
-        return {"value": merges / el, "unit": "merges/s", "cores": 1, "kind": "port",
-                "sample": "first %d docs of the config-2 batch, both directions, C oracle (oracle/awset_oracle.c, "
-                          "sorted-array restatement of awset.go:107-161), 1 thread, %d merges in %.1f s "
-                          "(no Go toolchain on the box: the reference itself cannot run)" % (n_sample, merges, el)}
+        return _cpu_baselines("first %d docs of the batch, A<-B and B<-A" % n_sample,
+                              lambda th, b: oracle.map_bench_join(ha, hb, True, th, b), run, 2 * n_sample, budget_s)
 
 
 class Config4(Config2):
@@ -158,9 +215,10 @@ class Config4(Config2):
     add/remove conflicts, full-state join both directions (BASELINE configs[3])."""
 
     R = 2
+    name = "config4"
     kernel = "join_block_kernel"
-    graph_ok = False  # worklist path (several kernels): eager launches
     metric = "replica-merges/sec (AWSet join, Zipf sizes, config 4) + achieved HBM GB/s (% roofline)"
+    cpu_docs = 96
 
     def __init__(self, eng, n, seed, dev, stream):
         import numpy as np
@@ -177,6 +235,7 @@ class Config4(Config2):
         self.total = int(offs[-1])
         self.d_offs = torch.from_numpy(offs.view(np.int32).copy()).to(dev)
         eng.reserve(n, 0)
+        eng.set_max_doc_entries()  # no size promise: documents up to 2^20 entries
         self.A = OutBuffers(n, R, self.total, device=dev)
         self.B = OutBuffers(n, R, self.total, device=dev)
         eng.gen_zipf_async(seed, n, self.d_offs, self.A, self.B, stream=stream)
@@ -190,15 +249,15 @@ class Config4(Config2):
 
     def describe(self, world):
         return {"workload": "config4: %d docs/GPU, Zipf(1.1)-like sizes in [1, 2^20) (mean %.0f, max %d, %d entries "
-                            "per side), 50%% concurrent add/remove conflicts, R=2, full-state join both directions"
-                            % (self.n, self.sizes.mean(), self.sizes.max(), self.total),
+                            "per side), 50%% concurrent add/remove conflicts, R=2, full-state join: A<-B and B<-A of "
+                            "one snapshot" % (self.n, self.sizes.mean(), self.sizes.max(), self.total),
                 "docs_per_gpu": self.n, "R": self.R, "entries_per_side": self.total,
                 "merges_per_step": self.merges_per_step * world, "parallelism": "doc-sharded x%d" % world}
 
-    def cpu_baseline(self, n_sample, budget_s):
+    def cpu_baseline(self, budget_s):
         from oracle import oracle
 
-        n_sample = min(n_sample, 256)
+        n_sample = min(self.cpu_docs, self.n)
         ha, hb = _host_batch(self.A, n_sample, self.R), _host_batch(self.B, n_sample, self.R)
 
         def run():
@@ -206,10 +265,9 @@ class Config4(Config2):
             rc2, _ = oracle.join(hb, ha)
             assert rc1 == 0 and rc2 == 0
 
-        merges, el = _time_cpu(run, 2 * n_sample, budget_s)
-        return {"value": merges / el, "unit": "merges/s", "cores": 1, "kind": "port",
-                "sample": "first %d docs of the config-4 batch (%d entries per side), both directions, C oracle, "
-                          "1 thread, %d merges in %.1f s" % (n_sample, int(ha.offsets[-1]), merges, el)}
+        return _cpu_baselines("first %d docs of the batch (%d entries per side), A<-B and B<-A" % (
+            n_sample, int(ha.offsets[-1])), lambda th, b: oracle.map_bench_join(ha, hb, True, th, b), run,
+            2 * n_sample, budget_s)
 
 
 class Config3:
@@ -217,8 +275,12 @@ class Config3:
 
     R = 16
     M = 10
-    kernel = "fold_sort_kernel"
+    name = "config3"
+    kernel = "fold_pipe_kernel"
+    kernel_name = "fold_pipe_kernel<32, true> (per-document fold, delta)"
     metric = "replica-merges/sec (AWSetDelta fold, config 3) + achieved HBM GB/s (% roofline)"
+    mode = 1  # CRDT_FOLD_DELTA
+    cpu_docs = 32768
 
     def __init__(self, eng, n, seed, dev, stream):
         import torch
@@ -236,13 +298,13 @@ class Config3:
         self.d = self.D.as_batch()
         self.merges_per_step = n * M
 
-    mode = 1  # CRDT_FOLD_DELTA
-    graph_ok = False  # eager launches (graph replay of the fold path not validated yet)
-
     def hot(self, s):
         if not hasattr(self, "_cs"):
             self._cs = (self.d.c(), self.S.c(), self.out.c())
         self.eng.fold_async(self.mode, *self._cs, stream=s)
+
+    def outputs(self):
+        return _outs(self.out)
 
     def post(self, s):
         self.eng.causal_context_async(self.out.vv, self.n, self.R, self.ctx, stream=s)
@@ -255,8 +317,9 @@ class Config3:
         from crdtgpu import workloads
 
         n, M = self.n, self.M
-        return workloads.fold_bytes(self.D.counts.cpu().numpy(), self.out.counts.cpu().numpy(), n * M * 8,
-                                    n * M * 2, n * M, self.R)
+        b = workloads.fold_bytes(self.D.counts.cpu().numpy(), self.out.counts.cpu().numpy(), n * M * 8,
+                                 n * M * 2, n * M, self.R)
+        return b, b
 
     def describe(self, world):
         return {"workload": "config3: %d dst docs/GPU x 64 entries, R=16, %d ordered AWSetDelta sources per doc "
@@ -264,43 +327,35 @@ class Config3:
                 "docs_per_gpu": self.n, "deltas_per_doc": self.M, "R": self.R,
                 "merges_per_step": self.merges_per_step * world, "parallelism": "doc-sharded x%d" % world}
 
-    def cpu_baseline(self, n_sample, budget_s):
-        import numpy as np
-
-        import crdtgpu
-        from crdtgpu.batch import SrcBatch
+    def cpu_baseline(self, budget_s):
         from oracle import oracle
 
-        M, R, S = self.M, self.R, self.S
-        hd = _host_batch(self.D, n_sample, R)
-        k = n_sample * M
-        u32, u64 = np.uint32, np.uint64
-        hs = SrcBatch(R, _np_copy(S.doc_srcs, n_sample + 1, u32), _np_copy(S.src_actor, k, u32),
-                      _np_copy(S.vv, k * R, u64), _np_copy(S.entry_off, k + 1, u32), _np_copy(S.keys, k * 8, u64),
-                      _np_copy(S.actors, k * 8, u32), _np_copy(S.counters, k * 8, u64),
-                      _np_copy(S.tomb_off, k + 1, u32), _np_copy(S.tkeys, k * 2, u64),
-                      _np_copy(S.tactors, k * 2, u32), _np_copy(S.tcounters, k * 2, u64))
+        n_sample = min(self.cpu_docs, self.n)
+        hd = _host_batch(self.D, n_sample, self.R)
+        hs = _host_srcs(self.S, n_sample, self.R, self.M, 8, 2)
 
         def run():
-            rc, _ = oracle.fold(crdtgpu.CRDT_FOLD_DELTA, hd, hs)
+            rc, _ = oracle.fold(self.mode, hd, hs)
             assert rc == 0
 
-        merges, el = _time_cpu(run, k, budget_s)
-        return {"value": merges / el, "unit": "merges/s", "cores": 1, "kind": "port",
-                "sample": "first %d docs of the config-3 batch (%d deltas), C oracle (oracle/awset_oracle.c, "
-                          "restatement of awset-delta_test.go:51-166), 1 thread, %d merges in %.1f s" % (
-                              n_sample, k, merges, el)}
+        return _cpu_baselines("first %d docs of the batch (%d deltas)" % (n_sample, n_sample * self.M),
+                              lambda th, b: oracle.map_bench_fold(self.mode, hd, hs, th, b), run,
+                              n_sample * self.M, budget_s)
 
 
-class Config5:
+class Config5(Config3):
     """100M docs x 8 replicas over 8 GPUs (BASELINE configs[4]): per GPU 12.5M docs,
     8 AWSet states of 16 entries (R = 8) folded r0 <- r1 <- ... <- r7 (7 merges
     per doc), then the global causal context: per-GPU VV max + RCCL all-reduce."""
 
     R = P = 8
     E = 16
-    kernel = "fold_sort_kernel"
+    name = "config5"
+    kernel = "fold_pipe_kernel"
+    kernel_name = "fold_pipe_kernel<32, false> (per-document fold, awset)"
     metric = "replica-merges/sec (AWSet fold r0<-..<-r7, config 5) + achieved HBM GB/s (% roofline)"
+    mode = 0  # CRDT_FOLD_AWSET
+    cpu_docs = 32768
 
     def __init__(self, eng, n, seed, dev, stream):
         import torch
@@ -313,24 +368,19 @@ class Config5:
         self.S = SrcBuffers(R, n, n * (P - 1), n * (P - 1) * E, 0, device=dev)
         eng.gen_replicas_async(seed, n, P, E, self.D, self.S, stream=stream)
         self.out = OutBuffers(n, R, n * E * P, device=dev)
-        # a doc never exceeds 16 + 7*16 = 128 slots: it stays on the LDS wave path
+        # a doc never exceeds 16 + 7*16 = 128 slots: it stays on the wave path
         eng.reserve(n, 0)
         self.ctx = torch.zeros(R, dtype=torch.int64, device=dev)
         self.d = self.D.as_batch()
         self.merges_per_step = n * (P - 1)
 
-    mode = 0  # CRDT_FOLD_AWSET
-    graph_ok = False
-    hot = Config3.hot
-    post = Config3.post
-    launches_per_step = Config3.launches_per_step
-
     def bytes_per_launch(self):
         from crdtgpu import workloads
 
         n, P, E = self.n, self.P, self.E
-        return workloads.fold_bytes(self.D.counts.cpu().numpy(), self.out.counts.cpu().numpy(), n * (P - 1) * E, 0,
-                                    n * (P - 1), self.R)
+        b = workloads.fold_bytes(self.D.counts.cpu().numpy(), self.out.counts.cpu().numpy(), n * (P - 1) * E, 0,
+                                 n * (P - 1), self.R)
+        return b, b
 
     def describe(self, world):
         return {"workload": "config5: %d docs/GPU x 8 replicas x 16 entries, R=8, fold r0<-r1<-..<-r7 + global "
@@ -338,89 +388,82 @@ class Config5:
                 "docs_per_gpu": self.n, "replicas": self.P, "entries_per_replica": self.E, "R": self.R,
                 "merges_per_step": self.merges_per_step * world, "parallelism": "doc-sharded x%d" % world}
 
-    def cpu_baseline(self, n_sample, budget_s):
-        import numpy as np
-
-        import crdtgpu
-        from crdtgpu.batch import SrcBatch
+    def cpu_baseline(self, budget_s):
         from oracle import oracle
 
-        P, E, R, S = self.P, self.E, self.R, self.S
-        hd = _host_batch(self.D, n_sample, R)
-        k = n_sample * (P - 1)
-        u32, u64 = np.uint32, np.uint64
-        hs = SrcBatch(R, _np_copy(S.doc_srcs, n_sample + 1, u32), _np_copy(S.src_actor, k, u32),
-                      _np_copy(S.vv, k * R, u64), _np_copy(S.entry_off, k + 1, u32), _np_copy(S.keys, k * E, u64),
-                      _np_copy(S.actors, k * E, u32), _np_copy(S.counters, k * E, u64))
+        n_sample = min(self.cpu_docs, self.n)
+        hd = _host_batch(self.D, n_sample, self.R)
+        hs = _host_srcs(self.S, n_sample, self.R, self.P - 1, self.E, 0)
 
         def run():
-            rc, _ = oracle.fold(crdtgpu.CRDT_FOLD_AWSET, hd, hs)
+            rc, _ = oracle.fold(self.mode, hd, hs)
             assert rc == 0
 
-        merges, el = _time_cpu(run, k, budget_s)
-        return {"value": merges / el, "unit": "merges/s", "cores": 1, "kind": "port",
-                "sample": "first %d docs of the config-5 batch (%d merges per pass), C oracle (oracle/awset_oracle.c, "
-                          "restatement of awset.go:107-161), 1 thread, %d merges in %.1f s" % (n_sample, k, merges, el)}
+        return _cpu_baselines("first %d docs of the batch (%d merges per pass)" % (n_sample, n_sample * (self.P - 1)),
+                              lambda th, b: oracle.map_bench_fold(self.mode, hd, hs, th, b), run,
+                              n_sample * (self.P - 1), budget_s)
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--config", type=int, default=2, choices=[2, 3, 4, 5])
-    ap.add_argument("--docs", type=int, default=None,
-                    help="documents per GPU (default 1,048,576; config 5: 12,500,000 = 100M / 8)")
-    ap.add_argument("--seed", type=int, default=0x5EED)
-    ap.add_argument("--cpu-sample", type=int, default=65536)
-    ap.add_argument("--cpu-budget", type=float, default=12.0)
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--separate", action="store_true", help="configs 2/4: two join launches instead of one exchange")
-    ap.add_argument("--no-graph", action="store_true", help="launch eagerly instead of replaying a captured HIP graph")
-    ap.add_argument("--force-graph", action="store_true", help="replay a captured HIP graph for every config")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
-    args = ap.parse_args()
+CONFIGS = {2: Config2, 3: Config3, 4: Config4, 5: Config5}
+DEFAULT_DOCS = {2: 1 << 20, 3: 1 << 20, 4: 16_384, 5: 12_500_000}
 
+
+def _traffic(path, config, n, W):
+    """HBM bytes per launch of this kernel from the PMC passes (tools/pmc.sh ->
+    tools/traffic.py --emit), matched on config, docs and kernel instance."""
+    if not os.path.exists(path):
+        return None
+    try:
+        for e in json.load(open(path)):
+            if (e.get("docs") == n and e.get("config") == config and e.get("kernel", "").startswith(W.kernel)
+                    and bool(e.get("exchange")) == bool(getattr(W, "exchange", False))):
+                return e.get("hbm_bytes_per_launch")
+    except Exception:
+        return None
+    return None
+
+
+def run_config(config, n, args, ctx, steps, warmup, repeats, cpu):
+    """Build one workload, time it, and return its result dict (the bench line's
+    fields).  Inputs are generated on the device before any timing."""
     import numpy as np
     import torch
 
-    import crdtgpu
     from crdtgpu.dist import u64_max_allreduce
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
-    torch.cuda.set_device(dev)
-    stream = torch.cuda.current_stream()
-
-    n = args.docs or {5: 12_500_000, 4: 16_384}.get(args.config, 1 << 20)
-    eng = crdtgpu.Engine(local)
-    # each rank owns its own documents (weak scaling; no data-path exchange)
-    seed = args.seed + (rank << 40)
-    cls = {2: Config2, 3: Config3, 4: Config4, 5: Config5}[args.config]
-    if args.separate:
+    eng, dev, stream, dist, world, rank = ctx
+    seed = args.seed + (rank << 40)  # each rank owns its own documents (weak scaling)
+    cls = CONFIGS[config]
+    if args.separate and config in (2, 4):
         cls.exchange = False
     W = cls(eng, n, seed, dev, stream)
     eng.sync(stream)
 
     # The dominant launch is captured once into a HIP graph and replayed each
-    # step: one host call per step instead of the ctypes/ABI calls of every
-    # kernel, so a loaded host cannot stretch the step.
-    graph = None
-    if not args.no_graph and (W.graph_ok or args.force_graph):
-        W.hot(stream)  # warm the workspaces before capture (no allocation inside)
-        torch.cuda.synchronize()
-        graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph):
-            W.hot(torch.cuda.current_stream())
-        torch.cuda.synchronize()
+    # step: one host call per step instead of the ABI calls of every kernel.
+    # Before timing, the replayed output is compared bitwise with an eager launch.
+    graph, replay_check, graph_error = None, None, None
+    if not args.no_graph:
+        try:
+            for t in W.outputs():  # poison, so a replay that writes nothing cannot pass
+                t.fill_(-1)
+            W.hot(stream)  # eager launch; also warms the workspaces (no allocation during capture)
+            torch.cuda.synchronize()
+            eager = [t.clone() for t in W.outputs()]
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                W.hot(torch.cuda.current_stream())
+            torch.cuda.synchronize()
+            for t in W.outputs():
+                t.fill_(-1)
+            g.replay()
+            torch.cuda.synchronize()
+            replay_check = all(bool(torch.equal(a, b)) for a, b in zip(eager, W.outputs()))
+            del eager
+            graph = g
+        except Exception as e:  # capture refused: report it and launch eagerly
+            graph_error = "%s: %s" % (type(e).__name__, e)
+            torch.cuda.synchronize()
 
     def step(ev=None):
         if ev is not None:
@@ -436,69 +479,45 @@ def main():
             return u64_max_allreduce(dist, local_ctx)
         return local_ctx
 
-    for _ in range(args.warmup):
+    for _ in range(warmup):
         step()
     eng.sync(stream)
-    bytes_launch = W.bytes_per_launch()  # algorithmic bytes from the actual output sizes
+    bytes_launch, per_merge_bytes = W.bytes_per_launch()  # from the actual output sizes
 
-    events = [[torch.cuda.Event(enable_timing=True) for _ in range(2)] for _ in range(args.steps)]
-    if dist is not None:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    g = None
-    for k in range(args.steps):
-        g = step(events[k])
-    torch.cuda.synchronize()
-    if dist is not None:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
+    def timed():
+        events = [[torch.cuda.Event(enable_timing=True) for _ in range(2)] for _ in range(steps)]
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        g = None
+        for k in range(steps):
+            g = step(events[k])
+        torch.cuda.synchronize()
+        if dist is not None:
+            dist.barrier()
+        el = time.perf_counter() - t0
+        if dist is not None:
+            t = torch.tensor([el], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el = float(t.item())
+        # mean duration of one launch of the dominant kernel, HIP events on its stream
+        tl = sum(e[0].elapsed_time(e[1]) for e in events) / steps / 1e3 / W.launches_per_step()
+        return el, tl, g
+
+    elapsed, t_launch, g = timed()
+    extra = [timed()[:2] for _ in range(max(0, repeats - 1))]
     eng.sync(stream)
-    replay_check = None
-    if graph is not None and hasattr(W, "out"):
-        # graph-replayed output vs an eager launch of the same call (bitwise)
-        snap = [t.clone() for t in (W.out.counts, W.out.keys, W.out.actors, W.out.counters, W.out.vv)]
-        W.hot(stream)
-        eng.sync(stream)
-        replay_check = all(bool(torch.equal(a, b)) for a, b in
-                           zip(snap, (W.out.counts, W.out.keys, W.out.actors, W.out.counters, W.out.vv)))
-        del snap
-    if dist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-
-    # mean duration of one launch of the dominant kernel, HIP events on its stream
-    t_launch = sum(e[0].elapsed_time(e[1]) for e in events) / args.steps / 1e3 / W.launches_per_step()
     achieved = bytes_launch / t_launch / 1e9
-    global_ctx = g.cpu().numpy().view(np.uint64).tolist() if g is not None else []
-
-    # HBM bytes per launch of this kernel from the PMC passes (tools/pmc.sh ->
-    # tools/traffic.py --emit), matched on config, docs and kernel instance
-    traffic = None
-    if os.path.exists(args.traffic_json):
-        try:
-            for e in json.load(open(args.traffic_json)):
-                if (e.get("docs") == n and e.get("config") == args.config and e.get("kernel", "").startswith(W.kernel)
-                        and bool(e.get("exchange")) == bool(getattr(W, "exchange", False))):
-                    traffic = e.get("hbm_bytes_per_launch")
-        except Exception:
-            traffic = None
-
-    merges = W.merges_per_step * world * args.steps
-    result = {
+    traffic = _traffic(args.traffic_json, config, n, W)
+    merges = W.merges_per_step * world * steps
+    res = {
         "metric": W.metric,
         "value": merges / elapsed,
         "unit": "merges/s",
-        "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": elapsed / args.steps * 1e3,
-        "higher_is_better": True,
-        "scaling": "weak",
-        "vs_baseline": None,
-        "dtype": "u64",
-        "data": "synthetic (AWSet states generated on device, csrc/gen.hip)",
+        "steps": steps,
+        "warmup": warmup,
+        "ms_per_step": elapsed / steps * 1e3,
         "launch": "hip graph replay" if graph is not None else "eager",
         "config": W.describe(world),
         "roofline": {
@@ -506,14 +525,95 @@ def main():
             "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": getattr(W, "kernel_name", W.kernel),
             "algorithmic_bytes_per_launch": bytes_launch, "launch_ms": t_launch * 1e3,
         },
-        "global_causal_context": global_ctx,
         "replay_check": replay_check,
+        "global_causal_context": g.cpu().numpy().view(np.uint64).tolist() if g is not None else [],
     }
+    if per_merge_bytes != bytes_launch:
+        res["roofline"]["survey_8d_per_merge_bytes"] = per_merge_bytes
+    if graph_error:
+        res["graph_error"] = graph_error
+    if extra:
+        res["repeats"] = [{"ms_per_step": e / steps * 1e3, "launch_ms": t * 1e3} for e, t in extra]
     if traffic:
-        result["roofline"]["traffic_gbs"] = traffic / t_launch / 1e9
-        result["roofline"]["traffic_frac"] = traffic / t_launch / 1e9 / HBM_PEAK_GBS
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        result["cpu_baseline"] = W.cpu_baseline(min(args.cpu_sample, n), args.cpu_budget)
+        res["roofline"]["traffic_gbs"] = traffic / t_launch / 1e9
+        res["roofline"]["traffic_frac"] = traffic / t_launch / 1e9 / HBM_PEAK_GBS
+    if cpu and rank == 0 and world == 1:
+        res["cpu_baseline"] = W.cpu_baseline(args.cpu_budget)
+    del graph, W
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    return res
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--config", type=int, default=2, choices=[2, 3, 4, 5], help="the headline workload")
+    ap.add_argument("--legs", default=None,
+                    help="comma-separated configs timed after the headline (default with --config 2: 3,4,5; "
+                         "otherwise none); 'none' for the headline only")
+    ap.add_argument("--leg-steps", type=int, default=20)
+    ap.add_argument("--leg-warmup", type=int, default=3)
+    ap.add_argument("--repeats", type=int, default=3, help="timed runs of the headline (the first is the value)")
+    ap.add_argument("--docs", type=int, default=None, help="documents per GPU for the headline")
+    ap.add_argument("--seed", type=int, default=0x5EED)
+    ap.add_argument("--cpu-budget", type=float, default=3.0, help="seconds per CPU baseline variant")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--separate", action="store_true", help="configs 2/4: two join launches instead of one exchange")
+    ap.add_argument("--no-graph", action="store_true", help="launch eagerly instead of replaying a captured HIP graph")
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
+    args = ap.parse_args()
+
+    import torch
+
+    import crdtgpu
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    stream = torch.cuda.current_stream()
+    eng = crdtgpu.Engine(local)
+    ctx = (eng, dev, stream, dist, world, rank)
+
+    if args.legs is None:
+        legs = [3, 4, 5] if args.config == 2 else []
+    elif args.legs == "none":
+        legs = []
+    else:
+        legs = [int(x) for x in args.legs.split(",") if x and int(x) != args.config]
+
+    n = args.docs or DEFAULT_DOCS[args.config]
+    head = run_config(args.config, n, args, ctx, args.steps, args.warmup, args.repeats, not args.no_cpu_baseline)
+    result = {
+        "metric": head.pop("metric"),
+        "value": head.pop("value"),
+        "unit": head.pop("unit"),
+        "n_gpus": world,
+        "steps": head.pop("steps"),
+        "warmup": head.pop("warmup"),
+        "ms_per_step": head.pop("ms_per_step"),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u64",
+        "data": "synthetic (AWSet states generated on device, csrc/gen.hip)",
+    }
+    result.update(head)
+    if legs:
+        result["legs"] = {}
+        for c in legs:
+            result["legs"]["config%d" % c] = run_config(c, DEFAULT_DOCS[c], args, ctx, args.leg_steps,
+                                                        args.leg_warmup, 1, not args.no_cpu_baseline)
     if rank == 0:
         print(json.dumps(result), flush=True)
     eng.close()

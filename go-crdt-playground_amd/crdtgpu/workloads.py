@@ -194,6 +194,14 @@ def join_bytes(n_dst, n_src, n_out, R) -> int:
     return int(20 * (n_dst.sum() + n_src.sum() + n_out.sum()) + (24 * R + 12) * n_dst.size)
 
 
+def exchange_bytes(n_a, n_b, n_ab, n_ba, R) -> int:
+    """One exchange launch (A <- B and B <- A from one read of both states):
+    Σ over docs of 20(n_a + n_b) read once + 20(n_ab + n_ba) written +
+    32R (two VVs read, two written) + 32 (offsets and counts: two read, two written)."""
+    n_a, n_b, n_ab, n_ba = (np.asarray(x, dtype=np.int64) for x in (n_a, n_b, n_ab, n_ba))
+    return int(20 * (n_a.sum() + n_b.sum() + n_ab.sum() + n_ba.sum()) + (32 * R + 32) * n_a.size)
+
+
 def fold_bytes(n_dst, n_out, src_entries, src_tombs, n_srcs_total, R) -> int:
     """Σ over docs of 20 n_dst + 8R + 4 + Σ_j [20 (c_j + x_j) + 8R + 12] + 20 n_out + 8R + 4."""
     n_dst, n_out = np.asarray(n_dst, dtype=np.int64), np.asarray(n_out, dtype=np.int64)

@@ -23,11 +23,12 @@ from crdtgpu.abi import CAWSetBatch, CAWSetOut, CSrcBatch  # noqa: E402
 from crdtgpu.batch import AWSetBatch, OutBuffers, SrcBatch  # noqa: E402
 
 LIB = os.path.join(HERE, "build", "liboracle.so")
+MAPLIB = os.path.join(HERE, "build", "libawsetmap.so")
 
 
 def build(force: bool = False) -> str:
-    if force or not os.path.exists(LIB):
-        subprocess.check_call(["make", "-s", "-C", HERE, "build/liboracle.so"])
+    if force or not os.path.exists(LIB) or not os.path.exists(MAPLIB):
+        subprocess.check_call(["make", "-s", "-C", HERE, "all"])
     return LIB
 
 
@@ -71,3 +72,79 @@ def causal_context(vv: np.ndarray, n_docs: int, R: int) -> np.ndarray:
     out = np.zeros(R, dtype=np.uint64)
     lib().oracle_causal_context(vv.ctypes.data, n_docs, R, out.ctypes.data)
     return out
+
+
+# ---- the map[string]Dot restatement (awset_map.cpp): second oracle + CPU baseline
+
+_maplib = None
+
+
+def maplib():
+    global _maplib
+    if _maplib is None:
+        build()
+        _maplib = ctypes.CDLL(MAPLIB)
+        P = ctypes.POINTER
+        m = _maplib
+        m.awmap_join.restype = ctypes.c_int
+        m.awmap_join.argtypes = [P(CAWSetBatch), P(CAWSetBatch), P(CAWSetOut)]
+        m.awmap_fold.restype = ctypes.c_int
+        m.awmap_fold.argtypes = [ctypes.c_int, P(CAWSetBatch), P(CSrcBatch), P(CAWSetOut)]
+        m.awmap_bench_join.restype = ctypes.c_double
+        m.awmap_bench_join.argtypes = [P(CAWSetBatch), P(CAWSetBatch), ctypes.c_int, ctypes.c_int, ctypes.c_double,
+                                       P(ctypes.c_uint64)]
+        m.awmap_bench_fold.restype = ctypes.c_double
+        m.awmap_bench_fold.argtypes = [ctypes.c_int, P(CAWSetBatch), P(CSrcBatch), ctypes.c_int, ctypes.c_double,
+                                       P(ctypes.c_uint64)]
+    return _maplib
+
+
+def map_join(dst: AWSetBatch, src: AWSetBatch):
+    """As join(), through the hash-map restatement."""
+    dst, src = dst.numpy(), src.numpy()
+    out = OutBuffers(dst.n_docs, dst.R, int(dst.offsets[-1]) + int(src.offsets[-1]))
+    d, s, o = dst.c(), src.c(), out.c()
+    rc = maplib().awmap_join(ctypes.byref(d), ctypes.byref(s), ctypes.byref(o))
+    return rc, out
+
+
+def map_fold(mode: int, dst: AWSetBatch, srcs: SrcBatch):
+    """As fold(), through the hash-map restatement."""
+    dst, srcs = dst.numpy(), srcs.numpy()
+    out = OutBuffers(dst.n_docs, dst.R, srcs.out_slots(dst))
+    d, s, o = dst.c(), srcs.c(), out.c()
+    rc = maplib().awmap_fold(int(mode), ctypes.byref(d), ctypes.byref(s), ctypes.byref(o))
+    return rc, out
+
+
+def map_bench_join(a: AWSetBatch, b: AWSetBatch, both_dirs: bool, threads: int, budget_s: float):
+    """(merges, timed seconds) of repeated map merges a <- b (and b <- a), maps cloned untimed per pass."""
+    a, b = a.numpy(), b.numpy()
+    ca, cb = a.c(), b.c()
+    m = ctypes.c_uint64(0)
+    t = maplib().awmap_bench_join(ctypes.byref(ca), ctypes.byref(cb), int(both_dirs), int(threads), float(budget_s),
+                                  ctypes.byref(m))
+    if t < 0:
+        raise RuntimeError("map baseline: a merge panicked (actor == len(VV))")
+    return int(m.value), t
+
+
+def map_bench_fold(mode: int, dst: AWSetBatch, srcs: SrcBatch, threads: int, budget_s: float):
+    """(merges, timed seconds) of repeated ordered map folds, dst maps cloned untimed per pass."""
+    dst, srcs = dst.numpy(), srcs.numpy()
+    cd, cs = dst.c(), srcs.c()
+    m = ctypes.c_uint64(0)
+    t = maplib().awmap_bench_fold(int(mode), ctypes.byref(cd), ctypes.byref(cs), int(threads), float(budget_s),
+                                  ctypes.byref(m))
+    if t < 0:
+        raise RuntimeError("map baseline: a merge panicked (actor == len(VV))")
+    return int(m.value), t
+
+
+def cpu_threads() -> int:
+    """Host threads a baseline may use: the affinity set, capped by OMP_NUM_THREADS when set."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    cap = os.environ.get("OMP_NUM_THREADS")
+    if cap and cap.isdigit() and int(cap) > 0:
+        n = min(n, int(cap))
+    return max(1, n)
