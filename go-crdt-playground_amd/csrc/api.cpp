@@ -6,6 +6,7 @@
 #include <cstdint>
 #include <cstring>
 #include <new>
+#include <vector>
 
 #include "../../include/crdtgpu.h"
 #include "crdt_device.hpp"
@@ -49,13 +50,21 @@ namespace {
 
 constexpr uint32_t kCtxParts = 1024;
 
-// Device buffer that only grows.
+// Device buffer that only grows.  A buffer it outgrows is retired, not freed:
+// a HIP graph captured earlier may still name it, so retired buffers live
+// until crdt_ctx_destroy.
 struct DevBuf {
     void* p = nullptr;
     size_t bytes = 0;
+    std::vector<void*>* retired = nullptr;
     int reserve(size_t want) {
         if (want <= bytes) return CRDT_OK;
-        if (p) (void)hipFree(p);
+        if (p) {
+            if (retired)
+                retired->push_back(p);
+            else
+                (void)hipFree(p);
+        }
         p = nullptr;
         bytes = 0;
         if (hipMalloc(&p, want) != hipSuccess) return CRDT_E_NOMEM;
@@ -91,6 +100,13 @@ struct crdt_ctx {
     // staging for the *_batch host path
     DevBuf stage[32];
     hipStream_t stream = nullptr;
+    // Ordering of the shared workspace across streams: the last call's stream
+    // and an event recorded after its launches.  A call on another stream
+    // waits for that event first (see enter()).
+    hipEvent_t last_ev = nullptr;
+    hipStream_t last_stream = nullptr;
+    bool has_last = false;
+    std::vector<void*> retired;  // outgrown workspace buffers, freed at destroy
 };
 
 namespace {
@@ -109,6 +125,38 @@ Work make_work(crdt_ctx* ctx) {
     w.chunk_ctr = ctx->ws.as<uint32_t>(32);
     w.worklist = ctx->worklist.as<uint32_t>();
     return w;
+}
+
+// Start of a call that uses the context's shared workspace (worklist,
+// counters, scratch, status word, context partials) on stream s.  Work of an
+// earlier call on a different stream is ordered before it with a stream wait
+// on that call's event.  While s is capturing a graph no wait is recorded
+// (the caller orders the capture; the capture itself must not allocate, see
+// grow()).
+int enter(crdt_ctx* ctx, hipStream_t s, bool& capturing) {
+    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(s, &st) != hipSuccess) return CRDT_E_HIP;
+    capturing = st != hipStreamCaptureStatusNone;
+    if (!capturing && ctx->has_last && ctx->last_stream != s)
+        if (hipStreamWaitEvent(s, ctx->last_ev, 0) != hipSuccess) return CRDT_E_HIP;
+    return CRDT_OK;
+}
+
+// End of such a call: its launches are what the next call on another stream waits for.
+int leave(crdt_ctx* ctx, hipStream_t s, bool capturing, int rc) {
+    if (rc != CRDT_OK || capturing) return rc;
+    if (hipEventRecord(ctx->last_ev, s) != hipSuccess) return CRDT_E_HIP;
+    ctx->last_stream = s;
+    ctx->has_last = true;
+    return CRDT_OK;
+}
+
+// Grow a workspace buffer; refused while capturing (an allocation would break
+// the capture, and the graph would keep the old address).
+int grow(DevBuf& b, size_t want, bool capturing) {
+    if (want <= b.bytes) return CRDT_OK;
+    if (capturing) return CRDT_E_WORKSPACE;
+    return b.reserve(want);
 }
 
 int reserve_worklist(crdt_ctx* ctx, uint32_t n_docs) {
@@ -174,6 +222,8 @@ int crdt_ctx_create(int device, crdt_ctx** out) {
     crdt_ctx* ctx = new (std::nothrow) crdt_ctx();
     if (!ctx) return CRDT_E_NOMEM;
     ctx->device = device;
+    for (DevBuf* b : {&ctx->ws, &ctx->worklist, &ctx->parts, &ctx->scratch}) b->retired = &ctx->retired;
+    for (auto& b : ctx->stage) b.retired = &ctx->retired;
     int rc = set_device(ctx);
     hipDeviceProp_t prop;
     if (rc == CRDT_OK && hipGetDeviceProperties(&prop, device) == hipSuccess) ctx->n_cu = prop.multiProcessorCount;
@@ -182,6 +232,7 @@ int crdt_ctx_create(int device, crdt_ctx** out) {
     if (rc == CRDT_OK) rc = reserve_worklist(ctx, 1024);
     if (rc == CRDT_OK) rc = ctx->parts.reserve((size_t)kCtxParts * CRDT_MAX_R * sizeof(uint64_t));
     if (rc == CRDT_OK) rc = hip_err(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
+    if (rc == CRDT_OK) rc = hip_err(hipEventCreateWithFlags(&ctx->last_ev, hipEventDisableTiming));
     if (rc != CRDT_OK) {
         crdt_ctx_destroy(ctx);
         return rc;
@@ -193,7 +244,12 @@ int crdt_ctx_create(int device, crdt_ctx** out) {
 void crdt_ctx_destroy(crdt_ctx* ctx) {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
+    if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    if (ctx->last_ev) (void)hipEventSynchronize(ctx->last_ev);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    if (ctx->last_ev) (void)hipEventDestroy(ctx->last_ev);
+    for (void* p : ctx->retired) (void)hipFree(p);
+    ctx->retired.clear();
     ctx->ws.release();
     ctx->worklist.release();
     ctx->parts.release();
@@ -236,6 +292,8 @@ int crdt_ctx_sync(crdt_ctx* ctx, void* stream) {
     if (rc != CRDT_OK) return rc;
     hipStream_t s = (hipStream_t)stream;
     if (hipStreamSynchronize(s) != hipSuccess) return CRDT_E_HIP;
+    // the status word is shared: also wait for the last call if it ran elsewhere
+    if (ctx->has_last && ctx->last_stream != s && hipEventSynchronize(ctx->last_ev) != hipSuccess) return CRDT_E_HIP;
     uint32_t status = 0;
     if (hipMemcpy(&status, ctx->ws.as<uint32_t>(64), sizeof(status), hipMemcpyDeviceToHost) != hipSuccess)
         return CRDT_E_HIP;
@@ -255,16 +313,20 @@ static int join_common(crdt_ctx* ctx, const crdt_awset_batch* dst, const crdt_aw
         return CRDT_E_INVALID;
     if (dst->n_docs != src->n_docs || dst->R != src->R) return CRDT_E_INVALID;
     int rc = set_device(ctx);
-    if (rc == CRDT_OK) rc = reserve_worklist(ctx, dst->n_docs);
     if (rc != CRDT_OK) return rc;
     hipStream_t s = (hipStream_t)stream;
+    bool cap = false;
+    rc = enter(ctx, s, cap);
+    if (rc == CRDT_OK) rc = grow(ctx->worklist, std::max<size_t>(dst->n_docs, 1) * sizeof(uint32_t), cap);
+    if (rc != CRDT_OK) return rc;
     const bool no_large = ctx->max_doc_entries <= 64;
     // the per-call counters are read only by the block path
     if (!no_large && launch_reset_work(ctx->ws.as<uint32_t>(0), s) != hipSuccess) return CRDT_E_HIP;
     OutView o2v;
     if (out2) o2v = view(out2);
-    return hip_err(launch_join(view(dst), view(src), view(out), out2 ? &o2v : nullptr, make_work(ctx),
-                               ctx->join_docs_per_wave, ctx->join_nt_stores, block_grid(ctx), no_large, s));
+    rc = hip_err(launch_join(view(dst), view(src), view(out), out2 ? &o2v : nullptr, make_work(ctx),
+                             ctx->join_docs_per_wave, ctx->join_nt_stores, block_grid(ctx), no_large, s));
+    return leave(ctx, s, cap, rc);
 }
 
 int crdt_awset_join_async(crdt_ctx* ctx, const crdt_awset_batch* dst, const crdt_awset_batch* src,
@@ -284,15 +346,22 @@ int crdt_awset_fold_async(crdt_ctx* ctx, int mode, const crdt_awset_batch* dst, 
     if (mode != CRDT_FOLD_AWSET && mode != CRDT_FOLD_DELTA) return CRDT_E_INVALID;
     if (dst->n_docs != srcs->n_docs || dst->R != srcs->R) return CRDT_E_INVALID;
     int rc = set_device(ctx);
-    if (rc == CRDT_OK) rc = reserve_worklist(ctx, dst->n_docs);
     if (rc != CRDT_OK) return rc;
-    if (ctx->scratch_slots == 0 && reserve_scratch(ctx, 1) != CRDT_OK) return CRDT_E_NOMEM;
     hipStream_t s = (hipStream_t)stream;
+    bool cap = false;
+    rc = enter(ctx, s, cap);
+    if (rc == CRDT_OK) rc = grow(ctx->worklist, std::max<size_t>(dst->n_docs, 1) * sizeof(uint32_t), cap);
+    if (rc != CRDT_OK) return rc;
+    if (ctx->scratch_slots == 0) {
+        if (cap) return CRDT_E_WORKSPACE;
+        if (reserve_scratch(ctx, 1) != CRDT_OK) return CRDT_E_NOMEM;
+    }
     if (launch_reset_work(ctx->ws.as<uint32_t>(0), s) != hipSuccess) return CRDT_E_HIP;
     const size_t slots = ctx->scratch_slots;
     Scratch scr{ctx->scratch.as<uint64_t>(0), ctx->scratch.as<uint32_t>(slots * 16), ctx->scratch.as<uint64_t>(slots * 8),
                 slots};
-    return hip_err(launch_fold(mode, view(dst), view(srcs), view(out), scr, make_work(ctx), block_grid(ctx), s));
+    rc = hip_err(launch_fold(mode, view(dst), view(srcs), view(out), scr, make_work(ctx), block_grid(ctx), s));
+    return leave(ctx, s, cap, rc);
 }
 
 int crdt_vv_max_async(crdt_ctx* ctx, uint64_t* dst, const uint64_t* src, size_t n, void* stream) {
@@ -308,7 +377,12 @@ int crdt_causal_context_async(crdt_ctx* ctx, const uint64_t* vv, uint32_t n_docs
     int rc = set_device(ctx);
     if (rc != CRDT_OK) return rc;
     uint32_t n_part = std::min<uint32_t>(kCtxParts, std::max<uint32_t>(1u, (n_docs + 255) / 256));
-    return hip_err(launch_context(vv, n_docs, R, ctx->parts.as<uint64_t>(), n_part, out, (hipStream_t)stream));
+    hipStream_t s = (hipStream_t)stream;
+    bool cap = false;
+    rc = enter(ctx, s, cap);
+    if (rc != CRDT_OK) return rc;
+    rc = hip_err(launch_context(vv, n_docs, R, ctx->parts.as<uint64_t>(), n_part, out, s));
+    return leave(ctx, s, cap, rc);
 }
 
 int crdt_gen_pair_async(crdt_ctx* ctx, uint64_t seed, uint32_t n_docs, const crdt_awset_out* a,

@@ -43,6 +43,17 @@
  * given HIP stream; crdt_ctx_sync returns device-side errors.  Device buffers
  * passed to *_async are caller-owned (device-resident, e.g. torch tensors).
  * The *_batch calls take host buffers and are synchronous.
+ *
+ * Streams and graphs: the calls of one context share its workspace (worklist,
+ * counters, fold scratch, status word).  A call issued on a different stream
+ * than the previous call of the same context first waits (hipStreamWaitEvent)
+ * for that call's launches, so calls of one context never overlap on the
+ * device, whatever streams they use; crdt_ctx_sync also waits for them.  A
+ * call made while its stream is capturing a HIP graph records no such wait
+ * (the capture is ordered by its caller) and never allocates: if the
+ * workspace would have to grow it returns CRDT_E_WORKSPACE (reserve first,
+ * or run the call once eagerly).  Buffers the workspace outgrows are kept
+ * until crdt_ctx_destroy, so graphs captured earlier stay valid.
  */
 #ifndef CRDTGPU_H
 #define CRDTGPU_H

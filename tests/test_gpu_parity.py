@@ -516,6 +516,80 @@ def test_config4_zipf_slice_exact(eng, torch):
         assert_same_all(host_out(o, torch), want, n, 2)
 
 
+def test_two_streams_share_one_context(eng, torch):
+    """A fold on one stream and a join on another, issued back to back on one
+    context with no host sync between: the context orders them (its workspace
+    -- worklist, counters, scratch, status -- is shared), so both are exact.
+    Large documents put both calls on the block path, which uses the worklist."""
+    rng = random.Random(61)
+    R = 3
+    fdst, fsrc = fold_case(rng, 120, R, lambda: rng.choice([100, 600]), lambda: rng.randint(1, 4),
+                           lambda: rng.choice([40, 300]), lambda: 0, 5000, 50, False)
+    jd = [random_state(rng, R, rng.choice([5, 900]), 4000, 30) for _ in range(150)]
+    js = [random_state(rng, R, rng.choice([5, 900]), 4000, 30) for _ in range(150)]
+    jdst, jsrc = batch_of(R, jd), batch_of(R, js)
+    rc1, want_f = oracle.fold(CRDT_FOLD_AWSET, fdst, fsrc)
+    rc2, want_j = oracle.join(jdst, jsrc)
+    assert rc1 == rc2 == 0
+    dev = torch.device("cuda:0")
+    fd, fs = fdst.to(dev), fsrc.to(dev)
+    jdd, jds = jdst.to(dev), jsrc.to(dev)
+    fout = OutBuffers(fdst.n_docs, R, fsrc.out_slots(fdst), device=dev)
+    jout = OutBuffers(jdst.n_docs, R, int(jdst.offsets[-1]) + int(jsrc.offsets[-1]), device=dev)
+    eng.reserve(max(fdst.n_docs, jdst.n_docs), fout.slots)
+    sa, sb = torch.cuda.Stream(), torch.cuda.Stream()
+    torch.cuda.synchronize()
+    for _ in range(3):
+        eng.fold_async(CRDT_FOLD_AWSET, fd, fs, fout, stream=sa)
+        eng.join_async(jdd, jds, jout, stream=sb)
+    eng.sync(sa)
+    eng.sync(sb)
+    assert_same(host_out(fout, torch), want_f, fdst.n_docs, R)
+    assert_same(host_out(jout, torch), want_j, jdst.n_docs, R)
+
+
+def test_capture_never_allocates_and_old_graphs_survive_growth(torch):
+    """While a stream captures, a call that would grow the workspace returns
+    CRDT_E_WORKSPACE; a graph captured before the workspace grows still replays
+    correctly afterwards (outgrown buffers are kept until destroy)."""
+    rng = random.Random(62)
+    R = 2
+    e = crdtgpu.Engine(0)
+    try:
+        dev = torch.device("cuda:0")
+        small = [random_state(rng, R, rng.randint(0, 90), 500, 9) for _ in range(600)]
+        small2 = [random_state(rng, R, rng.randint(0, 90), 500, 9) for _ in range(600)]
+        d1, s1 = batch_of(R, small), batch_of(R, small2)
+        rc, want = oracle.join(d1, s1)
+        assert rc == 0
+        dd, ds = d1.to(dev), s1.to(dev)
+        out = OutBuffers(d1.n_docs, R, int(d1.offsets[-1]) + int(s1.offsets[-1]), device=dev)
+        e.join_async(dd, ds, out, stream=torch.cuda.current_stream())  # sizes the workspace for 600 docs
+        e.sync(torch.cuda.current_stream())
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            e.join_async(dd, ds, out, stream=torch.cuda.current_stream())
+        # a bigger batch cannot be captured: it would need a bigger worklist
+        big = [random_state(rng, R, 3, 500, 9) for _ in range(5000)]
+        bd, bs = batch_of(R, big).to(dev), batch_of(R, big).to(dev)
+        bout = OutBuffers(5000, R, 6 * 5000, device=dev)
+        g2 = torch.cuda.CUDAGraph()
+        with pytest.raises(crdtgpu.CrdtError) as ei:
+            with torch.cuda.graph(g2):
+                e.join_async(bd, bs, bout, stream=torch.cuda.current_stream())
+        assert ei.value.code == crdtgpu.CRDT_E_WORKSPACE
+        # eagerly it grows the workspace; the first graph still replays correctly
+        e.join_async(bd, bs, bout, stream=torch.cuda.current_stream())
+        e.sync(torch.cuda.current_stream())
+        for t in (out.keys, out.actors, out.counters, out.vv, out.counts, out.offsets):
+            t.fill_(-1)
+        g.replay()
+        e.sync(torch.cuda.current_stream())
+        assert_same(host_out(out, torch), want, d1.n_docs, R)
+    finally:
+        e.close()
+
+
 @pytest.mark.parametrize("sizes", ["small", "mixed"])
 def test_exchange_equals_two_joins(eng, torch, sizes):
     """crdt_awset_exchange_*: one pass, out_ab = a <- b and out_ba = b <- a,
