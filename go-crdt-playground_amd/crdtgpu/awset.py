@@ -233,8 +233,32 @@ def _fold(mode, dsts, srcs_per_dst, engine):
                  _entries(getattr(s, "Deleted", None), ids)) for s in lst] for lst in srcs_per_dst]
     sb = SrcBatch.from_lists(R, per_doc)
     out = (engine or default_engine()).fold(mode, db, sb)
-    widths = [max([len(d.VersionVector)] + [len(s.VersionVector) for s in lst]) for d, lst in zip(dsts, srcs_per_dst)]
+    widths = [_fold_width(mode, d, lst) for d, lst in zip(dsts, srcs_per_dst)]
     _unpack(dsts, out, names, R, widths)
+
+
+def _fold_width(mode, dst, srcs) -> int:
+    """len(dst.VersionVector) after the fold, replayed on the VVs alone.  A
+    delta step that brings nothing (awset-delta_test.go:60) skips
+    VersionVector.Merge, so a longer source VV must not lengthen dst there; a
+    step merges iff Counter(src.Actor) == 0 (full merge, :53) or
+    MakeDeltaMergeData finds a changed entry or an effective tombstone
+    (:79-105) -- both decided by the VV before the step and the source alone."""
+    n = len(dst.VersionVector)
+    if mode != abi.CRDT_FOLD_DELTA:
+        return max([n] + [len(s.VersionVector) for s in srcs])
+    V = list(dst.VersionVector)
+    for s in srcs:
+        if (V[s.Actor] if s.Actor < len(V) else 0) != 0:
+            changed = any(not (d.Actor < len(V) and V[d.Actor] >= d.Counter) for d in s.Entries.values())
+            ents = s.Entries
+            eff = any(not (k in ents and (ents[k].Actor != d.Actor or ents[k].Counter > d.Counter))
+                      for k, d in (getattr(s, "Deleted", None) or {}).items())
+            if not changed and not eff:
+                continue
+        sv = list(s.VersionVector)
+        V = [max(x, y) for x, y in zip(V, sv)] + V[len(sv):] + sv[len(V):]
+    return len(V)
 
 
 def FoldBatch(dsts: Sequence[AWSet], srcs_per_dst: Sequence[Sequence[AWSet]], engine: Optional[Engine] = None):

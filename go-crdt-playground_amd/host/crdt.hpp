@@ -291,6 +291,42 @@ inline void MergeBatch(const std::vector<AWSet*>& dsts, const std::vector<const 
 }
 
 namespace detail {
+// len(dst.versionVector) after the fold, replayed on the VVs alone: a delta
+// step that brings nothing (awset-delta_test.go:60) skips VersionVector.Merge.
+// A step merges iff Counter(src.Actor) == 0 (:53) or MakeDeltaMergeData finds
+// a changed entry or an effective tombstone (:79-105).
+inline size_t fold_width(int mode, const AWSet& dst, const std::vector<const AWSet*>& srcs) {
+    size_t n = dst.versionVector.size();
+    if (mode != CRDT_FOLD_DELTA) {
+        for (auto* s : srcs) n = std::max(n, s->versionVector.size());
+        return n;
+    }
+    std::vector<uint64_t> V(dst.versionVector.begin(), dst.versionVector.end());
+    for (auto* s : srcs) {
+        if ((s->actor < V.size() ? V[s->actor] : 0) != 0) {
+            bool any = false;
+            for (auto& kv : s->entries)
+                if (!(kv.second.actor < V.size() && V[kv.second.actor] >= kv.second.counter)) any = true;
+            if (auto* del = s->deleted_map())
+                for (auto& kv : *del) {
+                    auto it = s->entries.find(kv.first);
+                    if (!(it != s->entries.end() &&
+                          (it->second.actor != kv.second.actor || it->second.counter > kv.second.counter)))
+                        any = true;
+                }
+            if (!any) continue;
+        }
+        const auto& sv = s->versionVector;
+        for (size_t i = 0; i < sv.size(); ++i) {
+            if (i < V.size())
+                V[i] = std::max(V[i], sv[i]);
+            else
+                V.push_back(sv[i]);
+        }
+    }
+    return V.size();
+}
+
 inline void fold(int mode, const std::vector<AWSet*>& dsts, const std::vector<std::vector<const AWSet*>>& srcs,
                  Engine& e) {
     if (dsts.size() != srcs.size()) throw Error(CRDT_E_INVALID, "fold: length mismatch");
@@ -326,11 +362,7 @@ inline void fold(int mode, const std::vector<AWSet*>& dsts, const std::vector<st
     Packed po = make_out(dsts.size(), b.R, pd.keys.size() + keys.size(), counts, co);
     check(crdt_awset_fold_batch(e.ctx(), mode, &cd, &cs, &co), "crdt_awset_fold_batch");
     std::vector<size_t> widths;
-    for (size_t i = 0; i < dsts.size(); ++i) {
-        size_t w = dsts[i]->versionVector.size();
-        for (auto* s : srcs[i]) w = std::max(w, s->versionVector.size());
-        widths.push_back(w);
-    }
+    for (size_t i = 0; i < dsts.size(); ++i) widths.push_back(fold_width(mode, *dsts[i], srcs[i]));
     b.unpack(dsts, po, counts, widths);
 }
 }  // namespace detail
