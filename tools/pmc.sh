@@ -25,7 +25,9 @@ if [ "${FOLD:-0}" = 1 ]; then
   pass lds2 SQ_LDS_IDX_ACTIVE SQ_LDS_ADDR_CONFLICT SQ_LDS_UNALIGNED_STALL SQ_INSTS_VMEM SQ_INST_LEVEL_LDS SQ_ACCUM_PREV_HIRES
   pass fetch FETCH_SIZE
   pass write WRITE_SIZE
-  python3 tools/traffic.py "$OUT" --docs ${DOCS:-1048576} > "$OUT/summary.txt"; cat "$OUT/summary.txt" | grep -A30 fold_pipe
+  cpass calib_fetch FETCH_SIZE
+  cpass calib_write WRITE_SIZE
+  python3 tools/traffic.py "$OUT" --docs ${DOCS:-1048576} --config ${CONFIG:-3} --kernel ${KERNEL:-fold_pipe_kernel} --emit > "$OUT/summary.txt"; cat "$OUT/summary.txt"
   exit 0
 fi
 pass fetch FETCH_SIZE
