@@ -216,7 +216,7 @@ class Config4(Config2):
 
     R = 2
     name = "config4"
-    kernel = "join_block_kernel"
+    kernel = "join_tile_kernel"
     metric = "replica-merges/sec (AWSet join, Zipf sizes, config 4) + achieved HBM GB/s (% roofline)"
     cpu_docs = 96
 
@@ -246,6 +246,11 @@ class Config4(Config2):
         self.a, self.b = self.A.as_batch(), self.B.as_batch()
         self.merges_per_step = 2 * n
         self.sizes = sizes
+
+    @property
+    def kernel_name(self):
+        return ("join_tile_kernel (exchange call: join_wave_kernel for docs <= 64 per side, tile plan, merge-path "
+                "tiles of 2048 positions with look-back placement; timed as the whole call)")
 
     def describe(self, world):
         return {"workload": "config4: %d docs/GPU, Zipf(1.1)-like sizes in [1, 2^20) (mean %.0f, max %d, %d entries "

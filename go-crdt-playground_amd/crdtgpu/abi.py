@@ -23,6 +23,8 @@ CRDT_E_CAPACITY = -4
 CRDT_E_HIP = -5
 CRDT_E_NOMEM = -6
 CRDT_E_WORKSPACE = -7
+CRDT_E_RCCL = -8
+CRDT_COMM_ID_BYTES = 128
 CRDT_MAX_R = 64
 CRDT_FOLD_AWSET = 0
 CRDT_FOLD_DELTA = 1
@@ -122,6 +124,10 @@ def _load():
         "crdt_awset_fold_batch": (ctypes.c_int, [_vp, ctypes.c_int, P(CAWSetBatch), P(CSrcBatch), P(CAWSetOut)]),
         "crdt_validate_batch": (ctypes.c_int, [P(CAWSetBatch)]),
         "crdt_validate_src_batch": (ctypes.c_int, [P(CSrcBatch)]),
+        "crdt_global_context_allreduce": (ctypes.c_int, [P(_vp), ctypes.c_int, P(_vp), _u32, _vp]),
+        "crdt_comm_unique_id": (ctypes.c_int, [_vp]),
+        "crdt_comm_init": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, _vp]),
+        "crdt_context_allreduce_async": (ctypes.c_int, [_vp, _vp, _u32, _vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)

@@ -85,6 +85,17 @@ class Engine:
         check(self._lib.crdt_causal_context_async(self._ctx, ptr(vv), int(n_docs), int(R), ptr(out),
                                                   _stream(stream)), "crdt_causal_context_async")
 
+    # -- multi-GPU: global causal context over RCCL ------------------------
+    def comm_init(self, n_ranks: int, rank: int, uid: bytes):
+        """One process per GPU: join the communicator of `uid` (crdt_comm_unique_id on rank 0)."""
+        buf = ctypes.create_string_buffer(bytes(uid), len(uid))
+        check(self._lib.crdt_comm_init(self._ctx, int(n_ranks), int(rank), buf), "crdt_comm_init")
+
+    def context_allreduce_async(self, vv_R, R: int, stream=None):
+        """In-place u64 max of this rank's R-vector with every other rank's (RCCL)."""
+        check(self._lib.crdt_context_allreduce_async(self._ctx, ptr(vv_R), int(R), _stream(stream)),
+              "crdt_context_allreduce_async")
+
     def gen_pair_async(self, seed: int, n_docs: int, a: OutBuffers, b: OutBuffers, stream=None):
         ca, cb = a.c(), b.c()
         check(self._lib.crdt_gen_pair_async(self._ctx, int(seed), int(n_docs), ctypes.byref(ca), ctypes.byref(cb),
@@ -131,6 +142,25 @@ class Engine:
         check(self._lib.crdt_awset_fold_batch(self._ctx, int(mode), ctypes.byref(d), ctypes.byref(s),
                                               ctypes.byref(o)), "crdt_awset_fold_batch")
         return out
+
+
+def comm_unique_id() -> bytes:
+    """A fresh RCCL communicator id (rank 0 makes it, every rank passes it to comm_init)."""
+    buf = ctypes.create_string_buffer(128)
+    check(abi.lib().crdt_comm_unique_id(buf), "crdt_comm_unique_id")
+    return buf.raw
+
+
+def global_context_allreduce(engines, vvs, R: int):
+    """One process, one Engine per GPU: every vvs[i] (device R-vector on engine i's
+    GPU) becomes the elementwise u64 max over all of them; returns it as a list."""
+    n = len(engines)
+    ctxs = (ctypes.c_void_p * n)(*[e._ctx for e in engines])
+    ptrs = (ctypes.c_void_p * n)(*[ptr(v) for v in vvs])
+    out = (ctypes.c_uint64 * int(R))()
+    check(abi.lib().crdt_global_context_allreduce(ctxs, n, ptrs, int(R), ctypes.cast(out, ctypes.c_void_p)),
+          "crdt_global_context_allreduce")
+    return [int(x) for x in out]
 
 
 def zipf_sizes(seed: int, n_docs: int):

@@ -14,7 +14,7 @@
 namespace crdt {
 hipError_t launch_join(const BatchView& dst, const BatchView& src, const OutView& out, const OutView* out2,
                        const Work& wk, uint32_t docs_per_wave, bool nt_stores, uint32_t block_grid, bool no_large,
-                       hipStream_t stream);
+                       const TileWork* tw, uint32_t n_cu, hipStream_t stream);
 hipError_t launch_fold(int mode, const BatchView& dst, const SrcView& sb, const OutView& out, const Scratch& scr,
                        const Work& wk, uint32_t block_grid, hipStream_t stream);
 hipError_t launch_vv_max(uint64_t* dst, const uint64_t* src, size_t n, hipStream_t stream);
@@ -93,6 +93,11 @@ struct crdt_ctx {
     DevBuf worklist;
     DevBuf parts;
     DevBuf scratch;  // fold block path ping-pong: keys | actors | counters
+    // large-document join tiles (tile.hip): descriptors + look-back words for
+    // tile_cap tiles, per-slot and per-run tile counts for the worklist
+    DevBuf tile_desc, tile_flags, tile_slot, tile_run;
+    uint32_t tile_cap = 1u << 20;             // crdt_ctx_set_option("join_tile_capacity")
+    bool join_tiles = true;                   // crdt_ctx_set_option("join_tiles")
     size_t scratch_slots = 0;
     uint32_t max_doc_entries = 0xFFFFFFFFu;  // caller's promise (crdt_ctx_set_max_doc_entries)
     uint32_t join_docs_per_wave = 8;          // crdt_ctx_set_option("join_docs_per_wave")
@@ -107,7 +112,21 @@ struct crdt_ctx {
     hipStream_t last_stream = nullptr;
     bool has_last = false;
     std::vector<void*> retired;  // outgrown workspace buffers, freed at destroy
+    void* comm = nullptr;        // RCCL communicator (comm.cpp)
+    void* comm_group = nullptr;  // single-process group it belongs to (comm.cpp)
 };
+
+void crdt_internal_comm_release(crdt_ctx* ctx);
+int crdt_internal_device(crdt_ctx* ctx) { return ctx->device; }
+hipStream_t crdt_internal_stream(crdt_ctx* ctx) { return ctx->stream; }
+void** crdt_internal_comm(crdt_ctx* ctx) { return &ctx->comm; }
+void** crdt_internal_comm_group(crdt_ctx* ctx) { return &ctx->comm_group; }
+// Order stream s after the context's last call (when that ran on another stream).
+int crdt_internal_order(crdt_ctx* ctx, hipStream_t s) {
+    if (ctx->has_last && ctx->last_stream != s && hipStreamWaitEvent(s, ctx->last_ev, 0) != hipSuccess)
+        return CRDT_E_HIP;
+    return CRDT_OK;
+}
 
 namespace {
 
@@ -212,6 +231,7 @@ const char* crdt_strerror(int code) {
         case CRDT_E_HIP: return "HIP runtime error";
         case CRDT_E_NOMEM: return "device allocation failed";
         case CRDT_E_WORKSPACE: return "fold scratch too small: call crdt_ctx_reserve with the output slot count";
+        case CRDT_E_RCCL: return "RCCL unavailable or a collective failed";
         default: return "unknown error";
     }
 }
@@ -222,7 +242,9 @@ int crdt_ctx_create(int device, crdt_ctx** out) {
     crdt_ctx* ctx = new (std::nothrow) crdt_ctx();
     if (!ctx) return CRDT_E_NOMEM;
     ctx->device = device;
-    for (DevBuf* b : {&ctx->ws, &ctx->worklist, &ctx->parts, &ctx->scratch}) b->retired = &ctx->retired;
+    for (DevBuf* b : {&ctx->ws, &ctx->worklist, &ctx->parts, &ctx->scratch, &ctx->tile_desc, &ctx->tile_flags,
+                      &ctx->tile_slot, &ctx->tile_run})
+        b->retired = &ctx->retired;
     for (auto& b : ctx->stage) b.retired = &ctx->retired;
     int rc = set_device(ctx);
     hipDeviceProp_t prop;
@@ -244,6 +266,7 @@ int crdt_ctx_create(int device, crdt_ctx** out) {
 void crdt_ctx_destroy(crdt_ctx* ctx) {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
+    crdt_internal_comm_release(ctx);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     if (ctx->last_ev) (void)hipEventSynchronize(ctx->last_ev);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
@@ -254,6 +277,7 @@ void crdt_ctx_destroy(crdt_ctx* ctx) {
     ctx->worklist.release();
     ctx->parts.release();
     ctx->scratch.release();
+    for (DevBuf* b : {&ctx->tile_desc, &ctx->tile_flags, &ctx->tile_slot, &ctx->tile_run}) b->release();
     for (auto& b : ctx->stage) b.release();
     delete ctx;
 }
@@ -277,6 +301,15 @@ int crdt_ctx_set_option(crdt_ctx* ctx, const char* name, int64_t value) {
     if (!strcmp(name, "join_docs_per_wave")) {
         if (value != 1 && value != 2 && value != 4 && value != 8 && value != 16) return CRDT_E_INVALID;
         ctx->join_docs_per_wave = (uint32_t)value;
+        return CRDT_OK;
+    }
+    if (!strcmp(name, "join_tile_capacity")) {  // tiles of 2048 merged positions; more -> block kernel
+        if (value < 1 || value > (1ll << 28)) return CRDT_E_INVALID;
+        ctx->tile_cap = (uint32_t)value;
+        return CRDT_OK;
+    }
+    if (!strcmp(name, "join_tiles")) {  // 0: large documents one workgroup each (join_block_kernel)
+        ctx->join_tiles = value != 0;
         return CRDT_OK;
     }
     if (!strcmp(name, "join_nt_stores")) {
@@ -320,12 +353,26 @@ static int join_common(crdt_ctx* ctx, const crdt_awset_batch* dst, const crdt_aw
     if (rc == CRDT_OK) rc = grow(ctx->worklist, std::max<size_t>(dst->n_docs, 1) * sizeof(uint32_t), cap);
     if (rc != CRDT_OK) return rc;
     const bool no_large = ctx->max_doc_entries <= 64;
-    // the per-call counters are read only by the block path
+    TileWork tw{};
+    const bool tiles = !no_large && ctx->join_tiles;
+    if (tiles) {
+        const size_t n = std::max<size_t>(dst->n_docs, 1);
+        rc = grow(ctx->tile_desc, (size_t)ctx->tile_cap * 16, cap);
+        if (rc == CRDT_OK) rc = grow(ctx->tile_flags, (size_t)ctx->tile_cap * 8, cap);
+        if (rc == CRDT_OK) rc = grow(ctx->tile_slot, n * 4, cap);
+        if (rc == CRDT_OK) rc = grow(ctx->tile_run, ((n + 1023) / 1024) * 4, cap);
+        if (rc != CRDT_OK) return rc;
+        uint32_t* w = ctx->ws.as<uint32_t>(0);
+        tw = TileWork{ctx->tile_desc.as<uint4>(), ctx->tile_flags.as<uint64_t>(), ctx->tile_slot.as<uint32_t>(),
+                      ctx->tile_run.as<uint32_t>(), w + 3, w + 4, w + 5, ctx->tile_cap};
+    }
+    // the per-call counters are read only by the large-document paths
     if (!no_large && launch_reset_work(ctx->ws.as<uint32_t>(0), s) != hipSuccess) return CRDT_E_HIP;
     OutView o2v;
     if (out2) o2v = view(out2);
     rc = hip_err(launch_join(view(dst), view(src), view(out), out2 ? &o2v : nullptr, make_work(ctx),
-                             ctx->join_docs_per_wave, ctx->join_nt_stores, block_grid(ctx), no_large, s));
+                             ctx->join_docs_per_wave, ctx->join_nt_stores, block_grid(ctx), no_large,
+                             tiles ? &tw : nullptr, (uint32_t)ctx->n_cu, s));
     return leave(ctx, s, cap, rc);
 }
 

@@ -72,6 +72,18 @@ struct Work {
     uint32_t* chunk_ctr;   // [8] chunk dispenser shards of the wave path
 };
 
+// Workspace of the large-document tile path (tile.hip).
+struct TileWork {
+    uint4* desc;          // [cap] {doc, tile index in doc, i0, j0}
+    uint64_t* flags;      // [cap] look-back words
+    uint32_t* slot_incl;  // [n_docs] inclusive tile count within the slot's run
+    uint32_t* run;        // [ceil(n_docs/kRun)] run sums -> exclusive prefixes
+    uint32_t* total;      // workspace word: tiles of this call
+    uint32_t* head;       // workspace word: tile dispenser
+    uint32_t* fallback;   // workspace word: 1 = tiles exceed cap, block kernel runs
+    uint32_t cap;
+};
+
 __device__ __forceinline__ uint32_t live_count(const uint32_t* offsets, const uint32_t* counts, uint32_t d) {
     return counts ? counts[d] : offsets[d + 1] - offsets[d];
 }

@@ -228,7 +228,9 @@ __global__ __launch_bounds__(WAVES * 64) void join_wave_kernel(BatchView dst, Ba
 // twice, once per direction).
 template <int NT, int IPT>
 __global__ __launch_bounds__(NT) void join_block_kernel(BatchView dst, BatchView src, OutView out, Work wk,
-                                                        uint32_t head) {
+                                                        uint32_t head, const uint32_t* gate) {
+    // gate != nullptr: the tile path (tile.hip) took the worklist unless it set *gate
+    if (gate && *gate == 0u) return;
     __shared__ MergeSmem<NT, IPT> sm;
     const uint32_t tid = threadIdx.x;
     const uint32_t R = dst.R;
@@ -293,9 +295,15 @@ static void launch_wave_k(uint32_t k, const BatchView& dst, const BatchView& src
 // output with non-temporal stores; no_large: the caller promised every doc has
 // <= 64 entries per side, so the block path is not launched (a larger doc then
 // raises CRDT_E_INVALID).  out2 != nullptr: exchange -- also out2 = src <- dst.
+hipError_t launch_join_tiles(const BatchView& A, const BatchView& B, const OutView& o1, const OutView* o2,
+                             const Work& wk, const TileWork& tw, uint32_t n_cu, hipStream_t stream);
+
+// tw != nullptr: large documents go through the merge-path tile path
+// (tile.hip); the per-document block kernel then only runs when the tiles
+// exceed the workspace (tw->fallback).
 hipError_t launch_join(const BatchView& dst, const BatchView& src, const OutView& out, const OutView* out2,
                        const Work& wk, uint32_t docs_per_wave, bool nt_stores, uint32_t block_grid, bool no_large,
-                       hipStream_t stream) {
+                       const TileWork* tw, uint32_t n_cu, hipStream_t stream) {
     if (dst.n_docs == 0) return hipSuccess;
     const OutView& o2 = out2 ? *out2 : out;
     if (out2) {
@@ -311,13 +319,19 @@ hipError_t launch_join(const BatchView& dst, const BatchView& src, const OutView
     }
     hipError_t e = hipGetLastError();
     if (e != hipSuccess || no_large) return e;
+    const uint32_t* gate = nullptr;
+    if (tw) {
+        e = launch_join_tiles(dst, src, out, out2, wk, *tw, n_cu, stream);
+        if (e != hipSuccess) return e;
+        gate = tw->fallback;
+    }
     hipLaunchKernelGGL((join_block_kernel<kBlockNT, kBlockIPT>), dim3(block_grid), dim3(kBlockNT), 0, stream, dst,
-                       src, out, wk, 0u);
+                       src, out, wk, 0u, gate);
     if (out2) {
         e = hipGetLastError();
         if (e != hipSuccess) return e;
         hipLaunchKernelGGL((join_block_kernel<kBlockNT, kBlockIPT>), dim3(block_grid), dim3(kBlockNT), 0, stream,
-                           src, dst, *out2, wk, 1u);
+                           src, dst, *out2, wk, 1u, gate);
     }
     return hipGetLastError();
 }

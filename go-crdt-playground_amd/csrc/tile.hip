@@ -1,0 +1,384 @@
+// Large-document join split across workgroups: merge-path tiles.
+//
+// (*AWSet).Merge (awset.go:103-161) of a document with up to millions of
+// entries per side.  The wave kernel (join.hip) pushes every document with
+// more than 64 entries on a side to the worklist; this path cuts each such
+// document into tiles of kTile merged positions so that one large document is
+// spread over the whole GPU instead of one workgroup:
+//
+//   tile_count_kernel   per worklist slot: tiles = ceil((nd + ns) / kTile),
+//                       inclusive scan within each run of 1024 slots
+//   tile_scan_kernel    one workgroup: exclusive scan of the run sums, the
+//                       total tile count; more tiles than the workspace holds
+//                       -> the per-document block kernel takes the worklist
+//   tile_split_kernel   one thread per tile: the tile's document and its
+//                       merge-path split (i0, j0) at diagonal t*kTile, found
+//                       by binary search over the two key arrays in HBM
+//   join_tile_kernel    persistent workgroups take tiles in order from an
+//                       atomic dispenser, stage the tile's dst and src runs in
+//                       LDS, decide every union key with the per-key rule,
+//                       place the survivors with a decoupled look-back prefix
+//                       within the document, and write them coalesced
+//
+// Merge order puts the dst element first on equal keys, so a common key's
+// pair is adjacent; a tile boundary may fall between the two.  The dst element
+// then peeks the first src element past its tile (staged at LDS index n), and
+// the src element sees the previous dst key (the element before i0).
+//
+// Exchange (EXCH): out1 = A <- B and out2 = B <- A from one read.  Both keep
+// the same keys at the same slots (join.hip, join_doc); only a common key's
+// dot differs, the src dot wins (awset.go:142), so each survivor stages two
+// LDS indices: the dot for out1 and the dot for out2.
+#include "crdt_device.hpp"
+#include "merge_block.hpp"
+
+namespace crdt {
+
+constexpr int kTileNT = 512;
+constexpr int kTileIPT = 4;
+constexpr uint32_t kTile = kTileNT * kTileIPT;  // merged positions per tile
+constexpr uint32_t kRun = 1024;                 // worklist slots per count/scan run
+
+// look-back word: status in bits 32-33, survivors in bits 0-31
+constexpr uint64_t kFlagAgg = 1ull << 32;
+constexpr uint64_t kFlagInc = 2ull << 32;
+
+
+__device__ __forceinline__ uint32_t doc_tiles(uint32_t nd, uint32_t ns) {
+    const uint32_t n = nd + ns;
+    return n == 0 ? 1u : (n + kTile - 1) / kTile;
+}
+
+template <int NT>
+__global__ __launch_bounds__(NT) void tile_count_kernel(BatchView A, BatchView B, Work wk, TileWork tw) {
+    __shared__ uint32_t wave_tot[NT / 64];
+    const uint32_t total_slots = work_total(wk, A.n_docs);
+    const uint32_t n_runs = (total_slots + kRun - 1) / kRun;
+    for (uint32_t r = blockIdx.x; r < n_runs; r += gridDim.x) {
+        uint32_t carry = 0;
+        for (uint32_t base = r * kRun; base < min((r + 1) * kRun, total_slots); base += NT) {
+            const uint32_t slot = base + threadIdx.x;
+            uint32_t n = 0;
+            if (slot < total_slots && slot < (r + 1) * kRun) {
+                const uint32_t d = wk.worklist[slot];
+                n = d < A.n_docs ? doc_tiles(live_count(A.offsets, A.counts, d), live_count(B.offsets, B.counts, d))
+                                 : 1u;
+            }
+            uint32_t tot;
+            const uint32_t ex = block_exclusive_scan<NT>(n, wave_tot, &tot);
+            if (slot < total_slots && slot < (r + 1) * kRun) tw.slot_incl[slot] = carry + ex + n;
+            carry += tot;
+        }
+        if (threadIdx.x == 0) tw.run[r] = carry;
+    }
+}
+
+template <int NT>
+__global__ __launch_bounds__(NT) void tile_scan_kernel(uint32_t n_docs, Work wk, TileWork tw) {
+    __shared__ uint32_t wave_tot[NT / 64];
+    const uint32_t total_slots = work_total(wk, n_docs);
+    const uint32_t n_runs = (total_slots + kRun - 1) / kRun;
+    uint64_t carry = 0;
+    for (uint32_t base = 0; base < n_runs; base += NT) {
+        const uint32_t r = base + threadIdx.x;
+        const uint32_t v = r < n_runs ? tw.run[r] : 0u;
+        uint32_t tot;
+        const uint32_t ex = block_exclusive_scan<NT>(v, wave_tot, &tot);
+        if (r < n_runs) tw.run[r] = (uint32_t)min<uint64_t>(carry + ex, 0xFFFFFFFFull);
+        carry += tot;
+    }
+    if (threadIdx.x == 0) {
+        const bool over = carry > tw.cap;
+        *tw.fallback = over ? 1u : 0u;
+        *tw.total = over ? 0u : (uint32_t)carry;
+    }
+}
+
+template <int NT>
+__global__ __launch_bounds__(NT) void tile_split_kernel(BatchView A, BatchView B, Work wk, TileWork tw) {
+    const uint32_t total = *tw.total;
+    const uint32_t total_slots = work_total(wk, A.n_docs);
+    const uint32_t n_runs = (total_slots + kRun - 1) / kRun;
+    for (uint32_t g = blockIdx.x * NT + threadIdx.x; g < total; g += gridDim.x * NT) {
+        // run: last r with run[r] <= g (run prefixes strictly increase: every slot has >= 1 tile)
+        uint32_t lo = 0, hi = n_runs;
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (tw.run[mid] <= g)
+                lo = mid;
+            else
+                hi = mid;
+        }
+        const uint32_t r = lo, rbase = tw.run[r], rel = g - rbase;
+        // slot: first slot of the run whose inclusive count exceeds rel
+        uint32_t s0 = r * kRun, s1 = min(s0 + kRun, total_slots);
+        while (s0 < s1) {
+            const uint32_t mid = (s0 + s1) >> 1;
+            if (tw.slot_incl[mid] <= rel)
+                s0 = mid + 1;
+            else
+                s1 = mid;
+        }
+        const uint32_t slot = s0;
+        const uint32_t first = (slot % kRun) ? tw.slot_incl[slot - 1] : 0u;
+        const uint32_t t = rel - first;
+        const uint32_t d = wk.worklist[slot];
+        uint32_t i0 = 0, j0 = 0;
+        if (d < A.n_docs) {
+            const uint32_t nd = live_count(A.offsets, A.counts, d), ns = live_count(B.offsets, B.counts, d);
+            const uint32_t k0 = min(t * kTile, nd + ns);
+            i0 = merge_path(A.keys + A.offsets[d], nd, B.keys + B.offsets[d], ns, k0);
+            j0 = k0 - i0;
+        }
+        tw.desc[g] = make_uint4(d, t, i0, j0);
+        tw.flags[g] = 0ull;
+    }
+}
+
+template <int NT, int IPT>
+struct TileSmem {
+    static constexpr uint32_t T = NT * IPT;
+    uint64_t key[T + 1];  // dst run at [0, nA), src run at [nA, nA+nB), peeked src element at nA+nB
+    uint64_t ctr[T + 1];
+    uint32_t act[T + 1];
+    uint32_t stage[T];  // survivor p: LDS index of its out1 dot | out2 dot << 16
+    uint64_t va[CRDT_MAX_R];
+    uint64_t vb[CRDT_MAX_R];
+    uint32_t wave_tot[NT / 64];
+    uint32_t word[4];
+    uint64_t prev_key;
+};
+
+__device__ __forceinline__ uint64_t flag_load(const uint64_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void flag_store(uint64_t* p, uint64_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Exclusive prefix of tile g (index t within its document) by decoupled
+// look-back over tiles g-1 .. g-t, 64 predecessors per poll (wave 0 only).
+// Tile 0 of a document publishes its inclusive count at once, so the walk
+// ends inside the document; a predecessor not yet published is polled again
+// (it was dispensed before g and publishes its aggregate without waiting).
+__device__ __forceinline__ uint32_t look_back(uint64_t* flags, uint32_t g, uint32_t t, uint32_t lane) {
+    uint32_t prefix = 0;
+    uint32_t look = g - 1;
+    int32_t rem = (int32_t)t;
+    for (;;) {
+        const uint64_t f = (int32_t)lane < rem ? flag_load(flags + (look - lane)) : kFlagInc;
+        const uint32_t st = (uint32_t)(f >> 32);
+        const uint64_t inc = ballot(st == 2u);
+        const uint32_t first_inc = inc ? (uint32_t)__builtin_ctzll(inc) : 64u;
+        const uint64_t pending = ballot(st == 0u) & low_mask(first_inc + 1u);
+        if (pending) {
+            __builtin_amdgcn_s_sleep(1);
+            continue;
+        }
+        uint32_t v = lane <= first_inc ? (uint32_t)f : 0u;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) v += (uint32_t)__shfl_xor((int)v, o);
+        prefix += v;
+        if (first_inc < 64u) break;
+        look -= 64;
+        rem -= 64;
+    }
+    return prefix;
+}
+
+template <int NT, int IPT, bool EXCH>
+__global__ __launch_bounds__(NT) void join_tile_kernel(BatchView A, BatchView B, OutView o1, OutView o2,
+                                                       TileWork tw, Work wk) {
+    __shared__ TileSmem<NT, IPT> sm;
+    constexpr uint32_t T = NT * IPT;
+    const uint32_t tid = threadIdx.x, lane = tid & 63;
+    const uint32_t R = A.R;
+    const uint32_t total = *tw.total;
+    uint32_t err = 0;
+    for (;;) {
+        if (tid == 0) sm.word[0] = atomicAdd(tw.head, 1u);
+        __syncthreads();
+        const uint32_t g = sm.word[0];
+        if (g >= total) break;
+        const uint4 ds = tw.desc[g];
+        const uint32_t d = ds.x, t = ds.y, i0 = ds.z, j0 = ds.w;
+        if (d >= A.n_docs) {  // not a document of this call: never dereferenced
+            if (tid == 0) {
+                atomicOr(wk.status, kErrWorkspace);
+                flag_store(tw.flags + g, kFlagInc);
+            }
+            __syncthreads();
+            continue;
+        }
+        const uint32_t nd = live_count(A.offsets, A.counts, d), ns = live_count(B.offsets, B.counts, d);
+        uint32_t i1 = nd, j1 = ns;
+        bool last = true;
+        if (g + 1 < total) {
+            const uint4 nx = tw.desc[g + 1];
+            if (nx.x == d && nx.y == t + 1) {
+                i1 = nx.z;
+                j1 = nx.w;
+                last = false;
+            }
+        }
+        const uint32_t nA = i1 - i0, nB = j1 - j0, n = nA + nB;  // n <= T
+        const uint32_t aoff = A.offsets[d], boff = B.offsets[d];
+        const uint64_t* ak = A.keys + aoff + i0;
+        const uint32_t* aa = A.actors + aoff + i0;
+        const uint64_t* ac = A.counters + aoff + i0;
+        const uint64_t* bk = B.keys + boff + j0;
+        const uint32_t* ba = B.actors + boff + j0;
+        const uint64_t* bc = B.counters + boff + j0;
+        // stage the tile: dst run, src run, then the src element past the tile
+        uint64_t rk[IPT], rc[IPT];
+        uint32_t ra[IPT];
+#pragma unroll
+        for (int q = 0; q < IPT; ++q) {
+            const uint32_t p = tid + q * NT;
+            const bool inA = p < nA;
+            const uint32_t pb = p - nA;
+            const bool inB = !inA && (p < n || (p == n && j1 < ns));
+            rk[q] = inA ? __builtin_nontemporal_load(ak + p) : (inB ? __builtin_nontemporal_load(bk + pb) : 0ull);
+            ra[q] = inA ? __builtin_nontemporal_load(aa + p) : (inB ? __builtin_nontemporal_load(ba + pb) : 0u);
+            rc[q] = inA ? __builtin_nontemporal_load(ac + p) : (inB ? __builtin_nontemporal_load(bc + pb) : 0ull);
+        }
+        // p == T (a full tile's peek) is not covered by the loop above
+        if (tid == 0) {
+            const bool peek = n == T && j1 < ns;
+            if (peek) {
+                sm.key[T] = bk[nB];
+                sm.act[T] = ba[nB];
+                sm.ctr[T] = bc[nB];
+            }
+            sm.word[2] = (j1 < ns) ? 1u : 0u;
+            sm.word[3] = i0 > 0 ? 1u : 0u;
+            sm.prev_key = i0 > 0 ? ak[-1] : 0ull;
+        }
+        if (tid < R) {
+            sm.va[tid] = A.vv[(size_t)d * R + tid];
+            sm.vb[tid] = B.vv[(size_t)d * R + tid];
+        }
+#pragma unroll
+        for (int q = 0; q < IPT; ++q) {
+            const uint32_t p = tid + q * NT;
+            if (p <= n && p < T) {
+                sm.key[p] = rk[q];
+                sm.act[p] = ra[q];
+                sm.ctr[p] = rc[q];
+            }
+        }
+        __syncthreads();
+        const bool has_next = sm.word[2] != 0, has_prev = sm.word[3] != 0;
+        const uint64_t prev_key = sm.prev_key;
+
+        // merge IPT positions from this thread's diagonal split
+        const uint32_t k0 = min(tid * IPT, n);
+        uint32_t a = merge_path(sm.key, nA, sm.key + nA, nB, k0);
+        uint32_t b = k0 - a;
+        uint32_t pick[IPT];
+        bool keep[IPT];
+        uint32_t cnt = 0;
+#pragma unroll
+        for (int q = 0; q < IPT; ++q) {
+            keep[q] = false;
+            pick[q] = 0;
+            if (k0 + q < n) {
+                const bool take_a = a < nA && (b >= nB || sm.key[a] <= sm.key[nA + b]);
+                if (take_a) {
+                    const uint64_t key = sm.key[a];
+                    const uint32_t nb = b < nB ? nA + b : n;  // next src element (peeked past the tile)
+                    const bool match = (b < nB || has_next) && sm.key[nb] == key;
+                    if (match) {  // common key: present, src dot wins (awset.go:123-129,142)
+                        keep[q] = true;
+                        pick[q] = nb | (a << 16);
+                    } else {  // dst-only: removed iff srcVV.HasDot(d) (awset.go:146-158)
+                        keep[q] = !has_dot(sm.vb, R, sm.act[a], sm.ctr[a], err);
+                        pick[q] = a | (a << 16);
+                    }
+                    ++a;
+                } else {
+                    const uint32_t sb = nA + b;
+                    const uint64_t key = sm.key[sb];
+                    const bool match = a > 0 ? sm.key[a - 1] == key : (has_prev && prev_key == key);
+                    if (!match) {  // src-only: added iff !dstVV.HasDot(s) (awset.go:130-140)
+                        keep[q] = !has_dot(sm.va, R, sm.act[sb], sm.ctr[sb], err);
+                        pick[q] = sb | (sb << 16);
+                    }
+                    ++b;
+                }
+                cnt += keep[q] ? 1u : 0u;
+            }
+        }
+        uint32_t agg;
+        const uint32_t lpos = block_exclusive_scan<NT>(cnt, sm.wave_tot, &agg);
+        {
+            uint32_t p = lpos;
+#pragma unroll
+            for (int q = 0; q < IPT; ++q)
+                if (keep[q]) sm.stage[p++] = pick[q];
+        }
+        if (tid < 64) {
+            uint32_t prefix = 0;
+            if (t == 0) {
+                if (lane == 0) flag_store(tw.flags + g, kFlagInc | agg);
+            } else {
+                if (lane == 0) flag_store(tw.flags + g, kFlagAgg | agg);
+                prefix = look_back(tw.flags, g, t, lane);
+                if (lane == 0) flag_store(tw.flags + g, kFlagInc | (prefix + agg));
+            }
+            if (lane == 0) sm.word[1] = prefix;
+        }
+        __syncthreads();
+        const uint32_t prefix = sm.word[1];
+        const size_t obase = (size_t)aoff + boff + prefix;
+        for (uint32_t p = tid; p < agg; p += NT) {
+            const uint32_t v = sm.stage[p];
+            const uint32_t x1 = v & 0xFFFFu, x2 = v >> 16;
+            const uint64_t key = sm.key[x1];
+            __builtin_nontemporal_store(key, o1.keys + obase + p);
+            __builtin_nontemporal_store(sm.act[x1], o1.actors + obase + p);
+            __builtin_nontemporal_store(sm.ctr[x1], o1.counters + obase + p);
+            if (EXCH) {
+                __builtin_nontemporal_store(key, o2.keys + obase + p);
+                __builtin_nontemporal_store(sm.act[x2], o2.actors + obase + p);
+                __builtin_nontemporal_store(sm.ctr[x2], o2.counters + obase + p);
+            }
+        }
+        if (last && tid == 0) {
+            o1.counts[d] = prefix + agg;
+            if (EXCH) o2.counts[d] = prefix + agg;
+        }
+        if (t == 0 && tid < R) {  // awset.go:160 -> crdt-misc.go:43-55, the same max both ways
+            const uint64_t m = max(sm.va[tid], sm.vb[tid]);
+            o1.vv[(size_t)d * R + tid] = m;
+            if (EXCH) o2.vv[(size_t)d * R + tid] = m;
+        }
+        __syncthreads();
+    }
+    if (__syncthreads_or(err != 0) && tid == 0) atomicOr(wk.status, kErrActorRange);
+}
+
+// Launch the tile path for the worklist the wave kernel filled.  n_cu sizes the
+// persistent grid.  out2 != nullptr: exchange.
+hipError_t launch_join_tiles(const BatchView& A, const BatchView& B, const OutView& o1, const OutView* o2,
+                             const Work& wk, const TileWork& tw, uint32_t n_cu, hipStream_t stream) {
+    const uint32_t n_runs = (A.n_docs + kRun - 1) / kRun;
+    hipLaunchKernelGGL((tile_count_kernel<256>), dim3(min(n_runs, 2048u)), dim3(256), 0, stream, A, B, wk, tw);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL((tile_scan_kernel<1024>), dim3(1), dim3(1024), 0, stream, A.n_docs, wk, tw);
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL((tile_split_kernel<256>), dim3(n_cu * 4), dim3(256), 0, stream, A, B, wk, tw);
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    if (o2)
+        hipLaunchKernelGGL((join_tile_kernel<kTileNT, kTileIPT, true>), dim3(n_cu * 3), dim3(kTileNT), 0, stream, A,
+                           B, o1, *o2, tw, wk);
+    else
+        hipLaunchKernelGGL((join_tile_kernel<kTileNT, kTileIPT, false>), dim3(n_cu * 3), dim3(kTileNT), 0, stream,
+                           A, B, o1, o1, tw, wk);
+    return hipGetLastError();
+}
+
+}  // namespace crdt

@@ -18,6 +18,10 @@
  *   crdt_causal_context_async
  *       the elementwise max over many version vectors (no reference
  *       counterpart: the per-GPU summary reduced across GPUs by RCCL)
+ *   crdt_global_context_allreduce / crdt_context_allreduce_async
+ *       that summary combined across GPUs: RCCL all-reduce(max, u64)
+ *       (the reference's counterpart is the CPU max over
+ *       every merged VersionVector, crdt-misc.go:43-55)
  *
  * HasDot (crdt-misc.go:28-34) and Counter (:36-41) run inside the kernels.
  *
@@ -76,6 +80,7 @@ extern "C" {
 #define CRDT_E_HIP (-5)         /* HIP runtime error                                   */
 #define CRDT_E_NOMEM (-6)       /* device allocation failed                            */
 #define CRDT_E_WORKSPACE (-7)   /* fold block path needs crdt_ctx_reserve(max_fold_slots) */
+#define CRDT_E_RCCL (-8)        /* RCCL not loadable, or a collective failed          */
 
 #define CRDT_MAX_R 64 /* version-vector length limit (one wave lane per actor) */
 
@@ -194,6 +199,30 @@ int crdt_gen_zipf_async(crdt_ctx* ctx, uint64_t seed, uint32_t n_docs, const uin
                         const crdt_awset_out* a, const crdt_awset_out* b, void* stream);
 int crdt_gen_replicas_async(crdt_ctx* ctx, uint64_t seed, uint32_t n_docs, uint32_t replicas, uint32_t entries,
                             const crdt_awset_out* dst, const crdt_src_batch* srcs, void* stream);
+
+/* ---- multi-GPU: the global causal context over RCCL (xGMI) --------------
+ * Documents shard over GPUs with no exchange; the one collective is the
+ * causal-context summary, R u64 per GPU, combined with
+ * ncclAllReduce(ncclUint64, ncclMax).  RCCL is bound at run time (an RCCL
+ * already mapped by the process is reused); without it these return
+ * CRDT_E_RCCL.
+ *
+ * One process, several GPUs: per_gpu[i] is a context on its own device and
+ * vv_R[i] a device pointer on that device holding its summary (e.g. the
+ * output of crdt_causal_context_async); every vv_R[i] is replaced by the
+ * elementwise max over all of them, and out_vv_R (host, may be NULL)
+ * receives a copy.  Synchronous.  The communicators are built on the first
+ * call and kept while the same contexts are passed in the same order.
+ *
+ * One process per GPU: rank 0 makes an id (crdt_comm_unique_id), every rank
+ * receives it out of band and calls crdt_comm_init; then
+ * crdt_context_allreduce_async reduces vv_R in place on `stream`. */
+#define CRDT_COMM_ID_BYTES 128
+int crdt_global_context_allreduce(crdt_ctx* const* per_gpu, int n_gpus, uint64_t* const* vv_R, uint32_t R,
+                                  uint64_t* out_vv_R);
+int crdt_comm_unique_id(uint8_t* id /* [CRDT_COMM_ID_BYTES] */);
+int crdt_comm_init(crdt_ctx* ctx, int n_ranks, int rank, const uint8_t* id);
+int crdt_context_allreduce_async(crdt_ctx* ctx, uint64_t* vv_R, uint32_t R, void* stream);
 
 /* ---- host buffers, synchronous: copies in, runs, copies out ------------- */
 int crdt_awset_join_batch(crdt_ctx* ctx, const crdt_awset_batch* dst, const crdt_awset_batch* src,
