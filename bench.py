@@ -550,6 +550,29 @@ def run_config(config, n, args, ctx, steps, warmup, repeats, cpu):
     return res
 
 
+def boundary_cost(n_docs):
+    """the host side of the drop-in, phase by phase (string
+    interning, SoA pack, H2D, exchange kernel, D2H, unpack to map[string]Dot),
+    through the C++ host mirror (tests/cpp/boundary_bench.cpp) on config-2-shaped
+    docs.  Never part of `value` (inputs there are already resident in HBM)."""
+    import subprocess
+
+    exe = os.path.join(ROOT, "go-crdt-playground_amd", "host", "build", "boundary_bench")
+    if not os.path.exists(exe):
+        return {"error": "boundary_bench not built (__graft_entry__.build())"}
+    try:
+        r = subprocess.run([exe, str(n_docs)], capture_output=True, text=True, timeout=300)
+        if r.returncode != 0:
+            return {"error": "exit %d: %s" % (r.returncode, r.stderr[-300:])}
+        out = json.loads(r.stdout.strip().splitlines()[-1])
+        out["what"] = ("C++ host mirror (go-crdt-playground_amd/host/crdt.hpp) around one exchange call: string keys "
+                       "interned to order-preserving ids, packed to SoA, copied H2D (pageable), both merges, D2H, "
+                       "rebuilt as unordered_map<string,Dot>; config-2-shaped docs")
+        return out
+    except Exception as e:  # reported, never fatal to the bench line
+        return {"error": "%s: %s" % (type(e).__name__, e)}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -568,6 +591,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--separate", action="store_true", help="configs 2/4: two join launches instead of one exchange")
     ap.add_argument("--no-graph", action="store_true", help="launch eagerly instead of replaying a captured HIP graph")
+    ap.add_argument("--no-boundary", action="store_true", help="skip the host boundary-cost leg")
+    ap.add_argument("--boundary-docs", type=int, default=65536)
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
     args = ap.parse_args()
 
@@ -619,6 +644,8 @@ def main():
         for c in legs:
             result["legs"]["config%d" % c] = run_config(c, DEFAULT_DOCS[c], args, ctx, args.leg_steps,
                                                         args.leg_warmup, 1, not args.no_cpu_baseline)
+    if rank == 0 and world == 1 and not args.no_boundary:
+        result["boundary"] = boundary_cost(args.boundary_docs)
     if rank == 0:
         print(json.dumps(result), flush=True)
     eng.close()

@@ -28,6 +28,11 @@ CRDT_COMM_ID_BYTES = 128
 CRDT_MAX_R = 64
 CRDT_FOLD_AWSET = 0
 CRDT_FOLD_DELTA = 1
+CRDT_OP_ADD = 0
+CRDT_OP_DEL = 1
+CRDT_OP_DELTA_DEL = 2
+CRDT_OP_DELTA_DEL_KEY = 3
+CRDT_MAX_OPS_PER_DOC = 256
 
 _vp = ctypes.c_void_p
 _u32 = ctypes.c_uint32
@@ -52,6 +57,18 @@ class CSrcBatch(ctypes.Structure):
         ("keys", _vp), ("actors", _vp), ("counters", _vp),
         ("tomb_off", _vp), ("tkeys", _vp), ("tactors", _vp), ("tcounters", _vp),
     ]
+
+
+class COpBatch(ctypes.Structure):
+    _fields_ = [("n_docs", _u32), ("op_off", _vp), ("kind", _vp), ("keys", _vp), ("doc_actor", _vp)]
+
+
+class CTombBatch(ctypes.Structure):
+    _fields_ = [("offsets", _vp), ("counts", _vp), ("keys", _vp), ("actors", _vp), ("counters", _vp)]
+
+
+class CTombOut(ctypes.Structure):
+    _fields_ = [("offsets", _vp), ("counts", _vp), ("keys", _vp), ("actors", _vp), ("counters", _vp)]
 
 
 class CrdtError(RuntimeError):
@@ -124,6 +141,17 @@ def _load():
         "crdt_awset_fold_batch": (ctypes.c_int, [_vp, ctypes.c_int, P(CAWSetBatch), P(CSrcBatch), P(CAWSetOut)]),
         "crdt_validate_batch": (ctypes.c_int, [P(CAWSetBatch)]),
         "crdt_validate_src_batch": (ctypes.c_int, [P(CSrcBatch)]),
+        "crdt_awset_apply_async": (ctypes.c_int, [_vp, P(CAWSetBatch), P(CTombBatch), P(COpBatch), P(CAWSetOut),
+                                                  P(CTombOut), _vp]),
+        "crdt_awset_apply_batch": (ctypes.c_int, [_vp, P(CAWSetBatch), P(CTombBatch), P(COpBatch), P(CAWSetOut),
+                                                  P(CTombOut)]),
+        "crdt_tombstone_gc_async": (ctypes.c_int, [_vp, P(CTombBatch), _u32, _u32, _vp, P(CTombOut), _vp]),
+        "crdt_vv_min_async": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_size_t, _vp]),
+        "crdt_awset_format": (ctypes.c_int, [P(CAWSetBatch), _u32, _vp, _vp, ctypes.c_size_t,
+                                             P(ctypes.c_size_t)]),
+        "crdt_batch_dump": (ctypes.c_int, [P(CAWSetBatch), _vp, ctypes.c_size_t, P(ctypes.c_size_t)]),
+        "crdt_batch_info": (ctypes.c_int, [_vp, ctypes.c_size_t, P(_u32), P(_u32), P(_u64)]),
+        "crdt_batch_undump": (ctypes.c_int, [_vp, ctypes.c_size_t, P(CAWSetOut)]),
         "crdt_global_context_allreduce": (ctypes.c_int, [P(_vp), ctypes.c_int, P(_vp), _u32, _vp]),
         "crdt_comm_unique_id": (ctypes.c_int, [_vp]),
         "crdt_comm_init": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, _vp]),

@@ -12,7 +12,7 @@ import ctypes
 
 import numpy as np
 
-from .abi import CAWSetBatch, CAWSetOut, CSrcBatch
+from .abi import CAWSetBatch, CAWSetOut, COpBatch, CSrcBatch, CTombBatch, CTombOut
 
 U32, U64 = np.uint32, np.uint64
 
@@ -49,7 +49,7 @@ def _torch(a, device):
         return None
     if _is_torch(a):
         return a.to(device)
-    sdt = {4: (np.int32, torch.int32), 8: (np.int64, torch.int64)}[a.dtype.itemsize]
+    sdt = {1: (np.uint8, torch.uint8), 4: (np.int32, torch.int32), 8: (np.int64, torch.int64)}[a.dtype.itemsize]
     return torch.from_numpy(np.ascontiguousarray(a).view(sdt[0])).to(device)
 
 
@@ -230,6 +230,101 @@ class SrcBuffers(SrcBatch):
                          z(n_srcs + 1, i32)[: n_srcs + 1], z(entry_slots, i64), z(entry_slots, i32),
                          z(entry_slots, i64), z(n_srcs + 1, i32)[: n_srcs + 1], z(tomb_slots, i64),
                          z(tomb_slots, i32), z(tomb_slots, i64))
+
+
+class OpBatch:
+    """Per doc an ordered list of local ops (include/crdtgpu.h, CRDT_OP_*) and
+    the doc's replica actor."""
+
+    def __init__(self, op_off, kind, keys, doc_actor):
+        self.op_off, self.kind, self.keys, self.doc_actor = op_off, kind, keys, doc_actor
+
+    @property
+    def n_docs(self) -> int:
+        return int(self.op_off.shape[0]) - 1
+
+    def c(self) -> COpBatch:
+        return COpBatch(self.n_docs, ptr(self.op_off), ptr(self.kind), ptr(self.keys), ptr(self.doc_actor))
+
+    def numpy(self) -> "OpBatch":
+        return OpBatch(_np(self.op_off, U32), _np(self.kind, np.uint8), _np(self.keys, U64),
+                       _np(self.doc_actor, U32))
+
+    def to(self, device) -> "OpBatch":
+        return OpBatch(*(_torch(a, device) for a in (self.op_off, self.kind, self.keys, self.doc_actor)))
+
+    @staticmethod
+    def from_lists(per_doc, actors) -> "OpBatch":
+        """per_doc[d] = [(kind, key)], actors[d] = the doc's replica actor."""
+        op_off = np.zeros(len(per_doc) + 1, dtype=U32)
+        np.cumsum([len(x) for x in per_doc], out=op_off[1:])
+        n = int(op_off[-1])
+        kind = np.zeros(max(n, 1), dtype=np.uint8)
+        keys = np.zeros(max(n, 1), dtype=U64)
+        i = 0
+        for lst in per_doc:
+            for k, key in lst:
+                kind[i], keys[i] = k, key
+                i += 1
+        return OpBatch(op_off, kind, keys, np.asarray(actors, dtype=U32).reshape(len(per_doc)))
+
+
+class TombBatch:
+    """AWSetDelta.Deleted of each doc: sorted (key, actor, counter) per doc."""
+
+    def __init__(self, offsets, keys, actors, counters, counts=None):
+        self.offsets, self.keys, self.actors, self.counters, self.counts = offsets, keys, actors, counters, counts
+
+    @property
+    def n_docs(self) -> int:
+        return int(self.offsets.shape[0]) - 1
+
+    def c(self) -> CTombBatch:
+        return CTombBatch(ptr(self.offsets), ptr(self.counts), ptr(self.keys), ptr(self.actors), ptr(self.counters))
+
+    def numpy(self) -> "TombBatch":
+        return TombBatch(_np(self.offsets, U32), _np(self.keys, U64), _np(self.actors, U32), _np(self.counters, U64),
+                         _np(self.counts, U32))
+
+    def to(self, device) -> "TombBatch":
+        return TombBatch(*(_torch(a, device) for a in (self.offsets, self.keys, self.actors, self.counters)),
+                         counts=_torch(self.counts, device))
+
+    @staticmethod
+    def from_lists(per_doc) -> "TombBatch":
+        offsets = np.zeros(len(per_doc) + 1, dtype=U32)
+        np.cumsum([len(x) for x in per_doc], out=offsets[1:])
+        n = int(offsets[-1])
+        k, a, c = np.zeros(max(n, 1), U64), np.zeros(max(n, 1), U32), np.zeros(max(n, 1), U64)
+        i = 0
+        for lst in per_doc:
+            for kk, aa, cc in lst:
+                k[i], a[i], c[i] = kk, aa, cc
+                i += 1
+        return TombBatch(offsets, k, a, c)
+
+    def doc(self, d):
+        o = int(self.offsets[d])
+        n = int(self.counts[d]) if self.counts is not None else int(self.offsets[d + 1]) - o
+        return list(zip(self.keys[o:o + n].tolist(), self.actors[o:o + n].tolist(), self.counters[o:o + n].tolist()))
+
+
+class TombBuffers(TombBatch):
+    """Output tombstones of an apply call (numpy, or torch on `device`)."""
+
+    def __init__(self, n_docs, slots, device=None):
+        if device is None:
+            super().__init__(np.zeros(n_docs + 1, U32), np.zeros(max(slots, 1), U64), np.zeros(max(slots, 1), U32),
+                             np.zeros(max(slots, 1), U64), np.zeros(max(n_docs, 1), U32)[:n_docs])
+        else:
+            import torch
+
+            e = lambda n, dt: torch.empty(max(n, 1), dtype=dt, device=device)  # noqa: E731
+            super().__init__(e(n_docs + 1, torch.int32)[: n_docs + 1], e(slots, torch.int64), e(slots, torch.int32),
+                             e(slots, torch.int64), e(n_docs, torch.int32)[:n_docs])
+
+    def c_out(self) -> CTombOut:
+        return CTombOut(ptr(self.offsets), ptr(self.counts), ptr(self.keys), ptr(self.actors), ptr(self.counters))
 
 
 def c_ref(x):

@@ -6,7 +6,7 @@ import ctypes
 
 from . import abi
 from .abi import check
-from .batch import AWSetBatch, OutBuffers, SrcBatch, ptr
+from .batch import AWSetBatch, OpBatch, OutBuffers, SrcBatch, TombBatch, TombBuffers, ptr
 
 
 def _c(x):
@@ -85,6 +85,27 @@ class Engine:
         check(self._lib.crdt_causal_context_async(self._ctx, ptr(vv), int(n_docs), int(R), ptr(out),
                                                   _stream(stream)), "crdt_causal_context_async")
 
+    def apply_async(self, state: AWSetBatch, ops: OpBatch, out: OutBuffers, tombs: TombBatch = None,
+                    tomb_out: TombBuffers = None, stream=None):
+        """Device-resident batched Add / Del / AWSetDelta.Del (crdt_awset_apply_async)."""
+        cs, co, cout = _c(state), _c(ops), _c(out)
+        ct = _c(tombs) if tombs is not None else None
+        cto = tomb_out.c_out() if tomb_out is not None else None
+        check(self._lib.crdt_awset_apply_async(self._ctx, ctypes.byref(cs), ctypes.byref(ct) if ct else None,
+                                               ctypes.byref(co), ctypes.byref(cout),
+                                               ctypes.byref(cto) if cto else None, _stream(stream)),
+              "crdt_awset_apply_async")
+
+    def tombstone_gc_async(self, tombs: TombBatch, R: int, stable_vv, out: TombBuffers, stream=None):
+        """Opt-in GC: drop each doc's tombstones its stable clock covers (crdt_tombstone_gc_async)."""
+        ct, co = _c(tombs), out.c_out()
+        check(self._lib.crdt_tombstone_gc_async(self._ctx, ctypes.byref(ct), tombs.n_docs, int(R), ptr(stable_vv),
+                                                ctypes.byref(co), _stream(stream)), "crdt_tombstone_gc_async")
+
+    def vv_min_async(self, dst, src, n: int, stream=None):
+        check(self._lib.crdt_vv_min_async(self._ctx, ptr(dst), ptr(src), int(n), _stream(stream)),
+              "crdt_vv_min_async")
+
     # -- multi-GPU: global causal context over RCCL ------------------------
     def comm_init(self, n_ranks: int, rank: int, uid: bytes):
         """One process per GPU: join the communicator of `uid` (crdt_comm_unique_id on rank 0)."""
@@ -135,6 +156,22 @@ class Engine:
                                                   ctypes.byref(c2)), "crdt_awset_exchange_batch")
         return o1, o2
 
+    def apply(self, state: AWSetBatch, ops: OpBatch, tombs: TombBatch = None, with_tombs: bool = True):
+        """Host buffers: (entries out, tombstones out or None) after each doc's ops."""
+        state, ops = state.numpy(), ops.numpy()
+        tombs = tombs.numpy() if tombs is not None else None
+        nops = int(ops.op_off[-1])
+        out = OutBuffers(state.n_docs, state.R, int(state.offsets[-1]) + nops)
+        tout = TombBuffers(state.n_docs, (int(tombs.offsets[-1]) if tombs is not None else 0) + nops) \
+            if with_tombs else None
+        cs, co, cout = state.c(), ops.c(), out.c()
+        ct = tombs.c() if tombs is not None else None
+        cto = tout.c_out() if tout is not None else None
+        check(self._lib.crdt_awset_apply_batch(self._ctx, ctypes.byref(cs), ctypes.byref(ct) if ct else None,
+                                               ctypes.byref(co), ctypes.byref(cout),
+                                               ctypes.byref(cto) if cto else None), "crdt_awset_apply_batch")
+        return out, tout
+
     def fold(self, mode: int, dst: AWSetBatch, srcs: SrcBatch) -> OutBuffers:
         dst, srcs = dst.numpy(), srcs.numpy()
         out = OutBuffers(dst.n_docs, dst.R, srcs.out_slots(dst))
@@ -161,6 +198,48 @@ def global_context_allreduce(engines, vvs, R: int):
     check(abi.lib().crdt_global_context_allreduce(ctxs, n, ptrs, int(R), ctypes.cast(out, ctypes.c_void_p)),
           "crdt_global_context_allreduce")
     return [int(x) for x in out]
+
+
+def format_doc(batch: AWSetBatch, d: int, names=None) -> str:
+    """Go's (AWSet).String() of doc d of a host batch (crdt_awset_format); names[id] = key string."""
+    b = batch.numpy()
+    cb = b.c()
+    arr = None
+    if names is not None:
+        enc = [n.encode() if isinstance(n, str) else bytes(n) for n in names]
+        arr = (ctypes.c_char_p * len(enc))(*enc)
+    n = ctypes.c_size_t(0)
+    check(abi.lib().crdt_awset_format(ctypes.byref(cb), int(d), arr, None, 0, ctypes.byref(n)), "crdt_awset_format")
+    buf = ctypes.create_string_buffer(n.value + 1)
+    check(abi.lib().crdt_awset_format(ctypes.byref(cb), int(d), arr, buf, n.value + 1, ctypes.byref(n)),
+          "crdt_awset_format")
+    return buf.raw[: n.value].decode("utf-8", errors="surrogateescape")
+
+
+def dump_batch(batch: AWSetBatch) -> bytes:
+    """Self-checking binary image of a host batch (crdt_batch_dump)."""
+    b = batch.numpy()
+    cb = b.c()
+    n = ctypes.c_size_t(0)
+    check(abi.lib().crdt_batch_dump(ctypes.byref(cb), None, 0, ctypes.byref(n)), "crdt_batch_dump")
+    buf = ctypes.create_string_buffer(n.value)
+    check(abi.lib().crdt_batch_dump(ctypes.byref(cb), buf, n.value, ctypes.byref(n)), "crdt_batch_dump")
+    return buf.raw
+
+
+def load_batch(image: bytes) -> AWSetBatch:
+    """Inverse of dump_batch: a compact host batch (crdt_batch_info + crdt_batch_undump)."""
+    import numpy as np
+
+    nd, R, ne = ctypes.c_uint32(0), ctypes.c_uint32(0), ctypes.c_uint64(0)
+    buf = ctypes.create_string_buffer(bytes(image), len(image))
+    check(abi.lib().crdt_batch_info(buf, len(image), ctypes.byref(nd), ctypes.byref(R), ctypes.byref(ne)),
+          "crdt_batch_info")
+    out = OutBuffers(nd.value, R.value, ne.value)
+    co = out.c()
+    check(abi.lib().crdt_batch_undump(buf, len(image), ctypes.byref(co)), "crdt_batch_undump")
+    return AWSetBatch(R.value, out.offsets, out.keys, out.actors, out.counters, out.vv,
+                      counts=out.counts if nd.value else np.zeros(0, np.uint32))
 
 
 def zipf_sizes(seed: int, n_docs: int):

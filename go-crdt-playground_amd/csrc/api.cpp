@@ -17,7 +17,13 @@ hipError_t launch_join(const BatchView& dst, const BatchView& src, const OutView
                        const TileWork* tw, uint32_t n_cu, hipStream_t stream);
 hipError_t launch_fold(int mode, const BatchView& dst, const SrcView& sb, const OutView& out, const Scratch& scr,
                        const Work& wk, uint32_t block_grid, hipStream_t stream);
+uint32_t tile_positions(uint32_t shape);
+hipError_t launch_apply(const BatchView& st, const TombView& tb, const ApplyOps& ops, const OutView& out,
+                        const TombOut& tout, bool has_tout, const Work& wk, uint32_t n_cu, hipStream_t stream);
 hipError_t launch_vv_max(uint64_t* dst, const uint64_t* src, size_t n, hipStream_t stream);
+hipError_t launch_vv_min(uint64_t* dst, const uint64_t* src, size_t n, hipStream_t stream);
+hipError_t launch_tomb_gc(const TombView& tb, uint32_t n_docs, uint32_t R, const uint64_t* stable, const TombOut& out,
+                          uint32_t n_cu, hipStream_t stream);
 hipError_t launch_reset_work(uint32_t* ws, hipStream_t stream);
 hipError_t launch_context(const uint64_t* vv, uint32_t n_docs, uint32_t R, uint64_t* part, uint32_t n_part,
                           uint64_t* out, hipStream_t stream);
@@ -98,6 +104,7 @@ struct crdt_ctx {
     DevBuf tile_desc, tile_flags, tile_slot, tile_run;
     uint32_t tile_cap = 1u << 20;             // crdt_ctx_set_option("join_tile_capacity")
     bool join_tiles = true;                   // crdt_ctx_set_option("join_tiles")
+    uint32_t tile_shape = 0;                  // crdt_ctx_set_option("join_tile_shape")
     size_t scratch_slots = 0;
     uint32_t max_doc_entries = 0xFFFFFFFFu;  // caller's promise (crdt_ctx_set_max_doc_entries)
     uint32_t join_docs_per_wave = 8;          // crdt_ctx_set_option("join_docs_per_wave")
@@ -308,6 +315,11 @@ int crdt_ctx_set_option(crdt_ctx* ctx, const char* name, int64_t value) {
         ctx->tile_cap = (uint32_t)value;
         return CRDT_OK;
     }
+    if (!strcmp(name, "join_tile_shape")) {  // 0: 512x4, 1: 256x4, 2: 256x8, 3: 1024x2 (threads x positions)
+        if (value < 0 || value > 3) return CRDT_E_INVALID;
+        ctx->tile_shape = (uint32_t)value;
+        return CRDT_OK;
+    }
     if (!strcmp(name, "join_tiles")) {  // 0: large documents one workgroup each (join_block_kernel)
         ctx->join_tiles = value != 0;
         return CRDT_OK;
@@ -364,7 +376,8 @@ static int join_common(crdt_ctx* ctx, const crdt_awset_batch* dst, const crdt_aw
         if (rc != CRDT_OK) return rc;
         uint32_t* w = ctx->ws.as<uint32_t>(0);
         tw = TileWork{ctx->tile_desc.as<uint4>(), ctx->tile_flags.as<uint64_t>(), ctx->tile_slot.as<uint32_t>(),
-                      ctx->tile_run.as<uint32_t>(), w + 3, w + 4, w + 5, ctx->tile_cap};
+                      ctx->tile_run.as<uint32_t>(), w + 3, w + 4, w + 5, ctx->tile_cap,
+                      tile_positions(ctx->tile_shape), ctx->tile_shape};
     }
     // the per-call counters are read only by the large-document paths
     if (!no_large && launch_reset_work(ctx->ws.as<uint32_t>(0), s) != hipSuccess) return CRDT_E_HIP;
@@ -409,6 +422,51 @@ int crdt_awset_fold_async(crdt_ctx* ctx, int mode, const crdt_awset_batch* dst, 
                 slots};
     rc = hip_err(launch_fold(mode, view(dst), view(srcs), view(out), scr, make_work(ctx), block_grid(ctx), s));
     return leave(ctx, s, cap, rc);
+}
+
+int crdt_awset_apply_async(crdt_ctx* ctx, const crdt_awset_batch* state, const crdt_tomb_batch* tombs,
+                           const crdt_op_batch* ops, const crdt_awset_out* out, const crdt_tomb_out* tomb_out,
+                           void* stream) {
+    if (!ctx || !batch_ptrs_ok(state) || !ops || !ops->op_off || !ops->doc_actor || !out_ptrs_ok(out))
+        return CRDT_E_INVALID;
+    if (ops->n_docs != state->n_docs) return CRDT_E_INVALID;
+    if (tombs && (!tombs->offsets || !tombs->keys || !tombs->actors || !tombs->counters)) return CRDT_E_INVALID;
+    if (tomb_out && (!tomb_out->offsets || !tomb_out->counts || !tomb_out->keys || !tomb_out->actors ||
+                     !tomb_out->counters))
+        return CRDT_E_INVALID;
+    int rc = set_device(ctx);
+    if (rc != CRDT_OK) return rc;
+    hipStream_t s = (hipStream_t)stream;
+    bool cap = false;
+    rc = enter(ctx, s, cap);
+    if (rc != CRDT_OK) return rc;
+    TombView tv{};
+    if (tombs) tv = TombView{tombs->offsets, tombs->counts, tombs->keys, tombs->actors, tombs->counters};
+    TombOut to{};
+    if (tomb_out) to = TombOut{tomb_out->offsets, tomb_out->counts, tomb_out->keys, tomb_out->actors, tomb_out->counters};
+    const ApplyOps av{ops->n_docs, ops->op_off, ops->kind, ops->keys, ops->doc_actor};
+    rc = hip_err(launch_apply(view(state), tv, av, view(out), to, tomb_out != nullptr, make_work(ctx),
+                              (uint32_t)ctx->n_cu, s));
+    return leave(ctx, s, cap, rc);
+}
+
+int crdt_vv_min_async(crdt_ctx* ctx, uint64_t* dst, const uint64_t* src, size_t n, void* stream) {
+    if (!ctx || (n && (!dst || !src))) return CRDT_E_INVALID;
+    int rc = set_device(ctx);
+    if (rc != CRDT_OK) return rc;
+    return hip_err(launch_vv_min(dst, src, n, (hipStream_t)stream));
+}
+
+int crdt_tombstone_gc_async(crdt_ctx* ctx, const crdt_tomb_batch* tombs, uint32_t n_docs, uint32_t R,
+                            const uint64_t* stable_vv, const crdt_tomb_out* out, void* stream) {
+    if (!ctx || !tombs || !tombs->offsets || !out || !out->offsets || !out->counts || R == 0 || R > CRDT_MAX_R ||
+        (n_docs && !stable_vv))
+        return CRDT_E_INVALID;
+    int rc = set_device(ctx);
+    if (rc != CRDT_OK) return rc;
+    const TombView tv{tombs->offsets, tombs->counts, tombs->keys, tombs->actors, tombs->counters};
+    const TombOut to{out->offsets, out->counts, out->keys, out->actors, out->counters};
+    return hip_err(launch_tomb_gc(tv, n_docs, R, stable_vv, to, (uint32_t)ctx->n_cu, (hipStream_t)stream));
 }
 
 int crdt_vv_max_async(crdt_ctx* ctx, uint64_t* dst, const uint64_t* src, size_t n, void* stream) {
@@ -595,6 +653,58 @@ int fetch_out(const crdt_awset_out* h, const crdt_awset_out& d, uint32_t n_docs,
 }  // namespace
 
 extern "C" {
+
+int crdt_awset_apply_batch(crdt_ctx* ctx, const crdt_awset_batch* state, const crdt_tomb_batch* tombs,
+                           const crdt_op_batch* ops, const crdt_awset_out* out, const crdt_tomb_out* tomb_out) {
+    if (!ctx || !ops || !ops->op_off || !ops->doc_actor || !out_ptrs_ok(out)) return CRDT_E_INVALID;
+    int rc = crdt_validate_batch(state);
+    if (rc != CRDT_OK) return rc;
+    if (ops->n_docs != state->n_docs) return CRDT_E_INVALID;
+    const uint32_t n = state->n_docs;
+    const size_t nops = ops->op_off[n];
+    if (nops && (!ops->kind || !ops->keys)) return CRDT_E_INVALID;
+    const uint64_t slots = (uint64_t)state->offsets[n] + nops;
+    const uint64_t tin = tombs ? tombs->offsets[n] : 0;
+    if (slots >= (1ull << 32) || tin + nops >= (1ull << 32)) return CRDT_E_INVALID;
+    if ((rc = set_device(ctx)) != CRDT_OK) return rc;
+    Stager st{ctx};
+    crdt_awset_batch ds = stage_batch(st, state);
+    crdt_op_batch dops = *ops;
+    dops.op_off = st.put(ops->op_off, (size_t)n + 1);
+    dops.kind = st.put(ops->kind, nops);
+    dops.keys = st.put(ops->keys, nops);
+    dops.doc_actor = st.put(ops->doc_actor, n);
+    crdt_tomb_batch dt{};
+    if (tombs) {
+        dt.offsets = st.put(tombs->offsets, (size_t)n + 1);
+        dt.counts = tombs->counts ? st.put(tombs->counts, n) : nullptr;
+        dt.keys = st.put(tombs->keys, tin);
+        dt.actors = st.put(tombs->actors, tin);
+        dt.counters = st.put(tombs->counters, tin);
+    }
+    crdt_awset_out dout = stage_out(st, n, state->R, slots);
+    crdt_tomb_out dto{};
+    if (tomb_out) {
+        dto.offsets = st.room<uint32_t>((size_t)n + 1);
+        dto.counts = st.room<uint32_t>(n);
+        dto.keys = st.room<uint64_t>(tin + nops);
+        dto.actors = st.room<uint32_t>(tin + nops);
+        dto.counters = st.room<uint64_t>(tin + nops);
+    }
+    if (st.rc != CRDT_OK) return st.rc;
+    rc = crdt_awset_apply_async(ctx, &ds, tombs ? &dt : nullptr, &dops, &dout, tomb_out ? &dto : nullptr,
+                                ctx->stream);
+    if (rc == CRDT_OK) rc = fetch_out(out, dout, n, state->R, slots, ctx->stream);
+    if (rc == CRDT_OK && tomb_out) {
+        rc = get(tomb_out->offsets, dto.offsets, (size_t)n + 1, ctx->stream);
+        if (rc == CRDT_OK) rc = get(tomb_out->counts, dto.counts, n, ctx->stream);
+        if (rc == CRDT_OK) rc = get(tomb_out->keys, dto.keys, tin + nops, ctx->stream);
+        if (rc == CRDT_OK) rc = get(tomb_out->actors, dto.actors, tin + nops, ctx->stream);
+        if (rc == CRDT_OK) rc = get(tomb_out->counters, dto.counters, tin + nops, ctx->stream);
+    }
+    const int sync = crdt_ctx_sync(ctx, ctx->stream);
+    return rc != CRDT_OK ? rc : sync;
+}
 
 int crdt_awset_join_batch(crdt_ctx* ctx, const crdt_awset_batch* dst, const crdt_awset_batch* src,
                           const crdt_awset_out* out) {

@@ -72,6 +72,31 @@ struct Work {
     uint32_t* chunk_ctr;   // [8] chunk dispenser shards of the wave path
 };
 
+// Batched local ops (apply.hip): the op lists, tombstones in and out.
+struct ApplyOps {
+    uint32_t n_docs;
+    const uint32_t* op_off;
+    const uint8_t* kind;
+    const uint64_t* keys;
+    const uint32_t* doc_actor;
+};
+
+struct TombView {  // AWSetDelta.Deleted of each doc (NULL offsets: none)
+    const uint32_t* offsets;
+    const uint32_t* counts;
+    const uint64_t* keys;
+    const uint32_t* actors;
+    const uint64_t* counters;
+};
+
+struct TombOut {
+    uint32_t* offsets;
+    uint32_t* counts;
+    uint64_t* keys;
+    uint32_t* actors;
+    uint64_t* counters;
+};
+
 // Workspace of the large-document tile path (tile.hip).
 struct TileWork {
     uint4* desc;          // [cap] {doc, tile index in doc, i0, j0}
@@ -82,6 +107,8 @@ struct TileWork {
     uint32_t* head;       // workspace word: tile dispenser
     uint32_t* fallback;   // workspace word: 1 = tiles exceed cap, block kernel runs
     uint32_t cap;
+    uint32_t tile;   // merged positions per tile (= the tile kernel's NT * IPT)
+    uint32_t shape;  // tile kernel shape (tile.hip, tile_positions)
 };
 
 __device__ __forceinline__ uint32_t live_count(const uint32_t* offsets, const uint32_t* counts, uint32_t d) {

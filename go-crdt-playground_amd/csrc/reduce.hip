@@ -83,6 +83,21 @@ hipError_t launch_reset_work(uint32_t* ws, hipStream_t stream) {
     return hipGetLastError();
 }
 
+__global__ void vv_min_kernel(uint64_t* dst, const uint64_t* src, size_t n) {
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+        const uint64_t a = dst[i], b = src[i];
+        dst[i] = a < b ? a : b;
+    }
+}
+
+hipError_t launch_vv_min(uint64_t* dst, const uint64_t* src, size_t n, hipStream_t stream) {
+    if (n == 0) return hipSuccess;
+    size_t grid = (n + 255) / 256;
+    if (grid > 4096) grid = 4096;
+    hipLaunchKernelGGL(vv_min_kernel, dim3((uint32_t)grid), dim3(256), 0, stream, dst, src, n);
+    return hipGetLastError();
+}
+
 hipError_t launch_vv_max(uint64_t* dst, const uint64_t* src, size_t n, hipStream_t stream) {
     if (n == 0) return hipSuccess;
     size_t grid = (n + 255) / 256;

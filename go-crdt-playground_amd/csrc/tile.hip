@@ -34,9 +34,6 @@
 
 namespace crdt {
 
-constexpr int kTileNT = 512;
-constexpr int kTileIPT = 4;
-constexpr uint32_t kTile = kTileNT * kTileIPT;  // merged positions per tile
 constexpr uint32_t kRun = 1024;                 // worklist slots per count/scan run
 
 // look-back word: status in bits 32-33, survivors in bits 0-31
@@ -44,9 +41,9 @@ constexpr uint64_t kFlagAgg = 1ull << 32;
 constexpr uint64_t kFlagInc = 2ull << 32;
 
 
-__device__ __forceinline__ uint32_t doc_tiles(uint32_t nd, uint32_t ns) {
+__device__ __forceinline__ uint32_t doc_tiles(uint32_t nd, uint32_t ns, uint32_t tile) {
     const uint32_t n = nd + ns;
-    return n == 0 ? 1u : (n + kTile - 1) / kTile;
+    return n == 0 ? 1u : (n + tile - 1) / tile;
 }
 
 template <int NT>
@@ -61,7 +58,8 @@ __global__ __launch_bounds__(NT) void tile_count_kernel(BatchView A, BatchView B
             uint32_t n = 0;
             if (slot < total_slots && slot < (r + 1) * kRun) {
                 const uint32_t d = wk.worklist[slot];
-                n = d < A.n_docs ? doc_tiles(live_count(A.offsets, A.counts, d), live_count(B.offsets, B.counts, d))
+                n = d < A.n_docs ? doc_tiles(live_count(A.offsets, A.counts, d), live_count(B.offsets, B.counts, d),
+                                             tw.tile)
                                  : 1u;
             }
             uint32_t tot;
@@ -126,7 +124,7 @@ __global__ __launch_bounds__(NT) void tile_split_kernel(BatchView A, BatchView B
         uint32_t i0 = 0, j0 = 0;
         if (d < A.n_docs) {
             const uint32_t nd = live_count(A.offsets, A.counts, d), ns = live_count(B.offsets, B.counts, d);
-            const uint32_t k0 = min(t * kTile, nd + ns);
+            const uint32_t k0 = min(t * tw.tile, nd + ns);
             i0 = merge_path(A.keys + A.offsets[d], nd, B.keys + B.offsets[d], ns, k0);
             j0 = k0 - i0;
         }
@@ -186,6 +184,88 @@ __device__ __forceinline__ uint32_t look_back(uint64_t* flags, uint32_t g, uint3
     return prefix;
 }
 
+// A tile's coordinates, from its descriptor and its successor's (uniform loads).
+struct TileGeo {
+    uint32_t d, t, i0, j0, nA, nB, ns, aoff, boff;
+    bool last, bad;
+};
+
+__device__ __forceinline__ TileGeo tile_geo(const BatchView& A, const BatchView& B, const TileWork& tw, uint32_t g,
+                                            uint32_t total) {
+    TileGeo x{};
+    const uint4 ds = tw.desc[g];
+    x.d = ds.x;
+    x.t = ds.y;
+    x.i0 = ds.z;
+    x.j0 = ds.w;
+    x.last = true;
+    x.bad = x.d >= A.n_docs;  // not a document of this call: never dereferenced
+    if (x.bad) return x;
+    const uint32_t nd = live_count(A.offsets, A.counts, x.d);
+    x.ns = live_count(B.offsets, B.counts, x.d);
+    x.aoff = A.offsets[x.d];
+    x.boff = B.offsets[x.d];
+    uint32_t i1 = nd, j1 = x.ns;
+    if (g + 1 < total) {
+        const uint4 nx = tw.desc[g + 1];
+        if (nx.x == x.d && nx.y == x.t + 1) {
+            i1 = nx.z;
+            j1 = nx.w;
+            x.last = false;
+        }
+    }
+    x.nA = i1 - x.i0;
+    x.nB = j1 - x.j0;
+    return x;
+}
+
+// Issue a tile's loads into registers.  Thread tid holds staged positions
+// p = tid + q*NT: the dst run [0, nA), the src run [nA, n), and at p == n the
+// src element past the tile (a common key's twin across the boundary).  The
+// last thread also fetches that element when the tile is full (p == T) and
+// the dst key just before the tile.
+template <int NT, int IPT>
+__device__ __forceinline__ void tile_issue(const BatchView& A, const BatchView& B, const TileGeo& x, uint32_t tid,
+                                           uint64_t (&rk)[IPT], uint32_t (&ra)[IPT], uint64_t (&rc)[IPT],
+                                           uint64_t& xk, uint32_t& xa, uint64_t& xc, uint64_t& pk) {
+    constexpr uint32_t T = NT * IPT;
+    const uint32_t n = x.nA + x.nB;
+    const bool peek = !x.bad && x.j0 + x.nB < x.ns;
+    const uint64_t* ak = A.keys + x.aoff + x.i0;
+    const uint32_t* aa = A.actors + x.aoff + x.i0;
+    const uint64_t* ac = A.counters + x.aoff + x.i0;
+    const uint64_t* bk = B.keys + x.boff + x.j0;
+    const uint32_t* ba = B.actors + x.boff + x.j0;
+    const uint64_t* bc = B.counters + x.boff + x.j0;
+#pragma unroll
+    for (int q = 0; q < IPT; ++q) {
+        const uint32_t p = tid + q * NT;
+        const bool inA = !x.bad && p < x.nA;
+        const uint32_t pb = p - x.nA;
+        const bool inB = !x.bad && !inA && (p < n || (p == n && peek));
+        rk[q] = inA ? __builtin_nontemporal_load(ak + p) : (inB ? __builtin_nontemporal_load(bk + pb) : 0ull);
+        ra[q] = inA ? __builtin_nontemporal_load(aa + p) : (inB ? __builtin_nontemporal_load(ba + pb) : 0u);
+        rc[q] = inA ? __builtin_nontemporal_load(ac + p) : (inB ? __builtin_nontemporal_load(bc + pb) : 0ull);
+    }
+    xk = 0;
+    xa = 0;
+    xc = 0;
+    pk = 0;
+    if (tid == NT - 1) {
+        if (n == T && peek) {
+            xk = bk[x.nB];
+            xa = ba[x.nB];
+            xc = bc[x.nB];
+        }
+        if (!x.bad && x.i0 > 0) pk = ak[-1];
+    }
+}
+
+// Persistent workgroups take tiles in order from an atomic dispenser.  The
+// next tile is taken once this tile's look-back is done (from then on nothing
+// of this tile waits on another workgroup, so a taken tile is never held
+// behind a wait), and its loads are issued before this tile's output stores,
+// which they overlap.
 template <int NT, int IPT, bool EXCH>
 __global__ __launch_bounds__(NT) void join_tile_kernel(BatchView A, BatchView B, OutView o1, OutView o2,
                                                        TileWork tw, Work wk) {
@@ -195,69 +275,22 @@ __global__ __launch_bounds__(NT) void join_tile_kernel(BatchView A, BatchView B,
     const uint32_t R = A.R;
     const uint32_t total = *tw.total;
     uint32_t err = 0;
-    for (;;) {
-        if (tid == 0) sm.word[0] = atomicAdd(tw.head, 1u);
-        __syncthreads();
-        const uint32_t g = sm.word[0];
-        if (g >= total) break;
-        const uint4 ds = tw.desc[g];
-        const uint32_t d = ds.x, t = ds.y, i0 = ds.z, j0 = ds.w;
-        if (d >= A.n_docs) {  // not a document of this call: never dereferenced
-            if (tid == 0) {
-                atomicOr(wk.status, kErrWorkspace);
-                flag_store(tw.flags + g, kFlagInc);
-            }
-            __syncthreads();
-            continue;
-        }
-        const uint32_t nd = live_count(A.offsets, A.counts, d), ns = live_count(B.offsets, B.counts, d);
-        uint32_t i1 = nd, j1 = ns;
-        bool last = true;
-        if (g + 1 < total) {
-            const uint4 nx = tw.desc[g + 1];
-            if (nx.x == d && nx.y == t + 1) {
-                i1 = nx.z;
-                j1 = nx.w;
-                last = false;
-            }
-        }
-        const uint32_t nA = i1 - i0, nB = j1 - j0, n = nA + nB;  // n <= T
-        const uint32_t aoff = A.offsets[d], boff = B.offsets[d];
-        const uint64_t* ak = A.keys + aoff + i0;
-        const uint32_t* aa = A.actors + aoff + i0;
-        const uint64_t* ac = A.counters + aoff + i0;
-        const uint64_t* bk = B.keys + boff + j0;
-        const uint32_t* ba = B.actors + boff + j0;
-        const uint64_t* bc = B.counters + boff + j0;
-        // stage the tile: dst run, src run, then the src element past the tile
-        uint64_t rk[IPT], rc[IPT];
-        uint32_t ra[IPT];
-#pragma unroll
-        for (int q = 0; q < IPT; ++q) {
-            const uint32_t p = tid + q * NT;
-            const bool inA = p < nA;
-            const uint32_t pb = p - nA;
-            const bool inB = !inA && (p < n || (p == n && j1 < ns));
-            rk[q] = inA ? __builtin_nontemporal_load(ak + p) : (inB ? __builtin_nontemporal_load(bk + pb) : 0ull);
-            ra[q] = inA ? __builtin_nontemporal_load(aa + p) : (inB ? __builtin_nontemporal_load(ba + pb) : 0u);
-            rc[q] = inA ? __builtin_nontemporal_load(ac + p) : (inB ? __builtin_nontemporal_load(bc + pb) : 0ull);
-        }
-        // p == T (a full tile's peek) is not covered by the loop above
-        if (tid == 0) {
-            const bool peek = n == T && j1 < ns;
-            if (peek) {
-                sm.key[T] = bk[nB];
-                sm.act[T] = ba[nB];
-                sm.ctr[T] = bc[nB];
-            }
-            sm.word[2] = (j1 < ns) ? 1u : 0u;
-            sm.word[3] = i0 > 0 ? 1u : 0u;
-            sm.prev_key = i0 > 0 ? ak[-1] : 0ull;
-        }
-        if (tid < R) {
-            sm.va[tid] = A.vv[(size_t)d * R + tid];
-            sm.vb[tid] = B.vv[(size_t)d * R + tid];
-        }
+    uint64_t rk[IPT], rc[IPT], xk, xc, pk;
+    uint32_t ra[IPT], xa;
+
+    if (tid == 0) sm.word[0] = atomicAdd(tw.head, 1u);
+    __syncthreads();
+    uint32_t g = sm.word[0];
+    TileGeo x{};
+    if (g < total) {
+        x = tile_geo(A, B, tw, g, total);
+        tile_issue<NT, IPT>(A, B, x, tid, rk, ra, rc, xk, xa, xc, pk);
+    }
+    while (g < total) {
+        const TileGeo cur = x;
+        const uint32_t nA = cur.nA, nB = cur.nB, n = nA + nB;  // n <= T
+        const uint32_t d = cur.d, t = cur.t;
+        // stage tile g: registers -> LDS
 #pragma unroll
         for (int q = 0; q < IPT; ++q) {
             const uint32_t p = tid + q * NT;
@@ -267,8 +300,20 @@ __global__ __launch_bounds__(NT) void join_tile_kernel(BatchView A, BatchView B,
                 sm.ctr[p] = rc[q];
             }
         }
+        if (tid == NT - 1) {
+            if (n == T) {
+                sm.key[T] = xk;
+                sm.act[T] = xa;
+                sm.ctr[T] = xc;
+            }
+            sm.prev_key = pk;
+        }
+        if (!cur.bad && tid < R) {
+            sm.va[tid] = A.vv[(size_t)d * R + tid];
+            sm.vb[tid] = B.vv[(size_t)d * R + tid];
+        }
         __syncthreads();
-        const bool has_next = sm.word[2] != 0, has_prev = sm.word[3] != 0;
+        const bool has_next = !cur.bad && cur.j0 + nB < cur.ns, has_prev = !cur.bad && cur.i0 > 0;
         const uint64_t prev_key = sm.prev_key;
 
         // merge IPT positions from this thread's diagonal split
@@ -319,43 +364,97 @@ __global__ __launch_bounds__(NT) void join_tile_kernel(BatchView A, BatchView B,
         }
         if (tid < 64) {
             uint32_t prefix = 0;
-            if (t == 0) {
+            if (cur.bad) {
+                if (lane == 0) {
+                    atomicOr(wk.status, kErrWorkspace);
+                    flag_store(tw.flags + g, kFlagInc);
+                }
+            } else if (t == 0) {
                 if (lane == 0) flag_store(tw.flags + g, kFlagInc | agg);
             } else {
                 if (lane == 0) flag_store(tw.flags + g, kFlagAgg | agg);
+            }
+            if (!cur.bad && t != 0) {
                 prefix = look_back(tw.flags, g, t, lane);
                 if (lane == 0) flag_store(tw.flags + g, kFlagInc | (prefix + agg));
             }
-            if (lane == 0) sm.word[1] = prefix;
+            // nothing of this tile waits on another workgroup any more: take the
+            // next tile now (a tile taken earlier would be held while this one's
+            // look-back waits, and its successors would wait on that in turn)
+            if (lane == 0) {
+                sm.word[0] = atomicAdd(tw.head, 1u);
+                sm.word[1] = prefix;
+            }
         }
         __syncthreads();
         const uint32_t prefix = sm.word[1];
-        const size_t obase = (size_t)aoff + boff + prefix;
-        for (uint32_t p = tid; p < agg; p += NT) {
-            const uint32_t v = sm.stage[p];
-            const uint32_t x1 = v & 0xFFFFu, x2 = v >> 16;
-            const uint64_t key = sm.key[x1];
-            __builtin_nontemporal_store(key, o1.keys + obase + p);
-            __builtin_nontemporal_store(sm.act[x1], o1.actors + obase + p);
-            __builtin_nontemporal_store(sm.ctr[x1], o1.counters + obase + p);
-            if (EXCH) {
-                __builtin_nontemporal_store(key, o2.keys + obase + p);
-                __builtin_nontemporal_store(sm.act[x2], o2.actors + obase + p);
-                __builtin_nontemporal_store(sm.ctr[x2], o2.counters + obase + p);
+        const uint32_t gn = sm.word[0];
+        if (gn < total) {  // the next tile's loads overlap this tile's stores
+            x = tile_geo(A, B, tw, gn, total);
+            tile_issue<NT, IPT>(A, B, x, tid, rk, ra, rc, xk, xa, xc, pk);
+        }
+        if (!cur.bad) {
+            const size_t obase = (size_t)cur.aoff + cur.boff + prefix;
+#pragma unroll
+            for (int q = 0; q < IPT; ++q) {
+                const uint32_t p = tid + q * NT;
+                if (p < agg) {
+                    const uint32_t v = sm.stage[p];
+                    const uint32_t x1 = v & 0xFFFFu, x2 = v >> 16;
+                    const uint64_t key = sm.key[x1];
+                    __builtin_nontemporal_store(key, o1.keys + obase + p);
+                    __builtin_nontemporal_store(sm.act[x1], o1.actors + obase + p);
+                    __builtin_nontemporal_store(sm.ctr[x1], o1.counters + obase + p);
+                    if (EXCH) {
+                        __builtin_nontemporal_store(key, o2.keys + obase + p);
+                        __builtin_nontemporal_store(sm.act[x2], o2.actors + obase + p);
+                        __builtin_nontemporal_store(sm.ctr[x2], o2.counters + obase + p);
+                    }
+                }
+            }
+            if (cur.last && tid == 0) {
+                o1.counts[d] = prefix + agg;
+                if (EXCH) o2.counts[d] = prefix + agg;
+            }
+            if (t == 0 && tid < R) {  // awset.go:160 -> crdt-misc.go:43-55, the same max both ways
+                const uint64_t m = max(sm.va[tid], sm.vb[tid]);
+                o1.vv[(size_t)d * R + tid] = m;
+                if (EXCH) o2.vv[(size_t)d * R + tid] = m;
             }
         }
-        if (last && tid == 0) {
-            o1.counts[d] = prefix + agg;
-            if (EXCH) o2.counts[d] = prefix + agg;
-        }
-        if (t == 0 && tid < R) {  // awset.go:160 -> crdt-misc.go:43-55, the same max both ways
-            const uint64_t m = max(sm.va[tid], sm.vb[tid]);
-            o1.vv[(size_t)d * R + tid] = m;
-            if (EXCH) o2.vv[(size_t)d * R + tid] = m;
-        }
         __syncthreads();
+        g = gn;
     }
     if (__syncthreads_or(err != 0) && tid == 0) atomicOr(wk.status, kErrActorRange);
+}
+
+// Tile shapes (workgroup size x positions per thread); "join_tile_shape".
+template <int NT, int IPT>
+static hipError_t launch_tile_kernel(const BatchView& A, const BatchView& B, const OutView& o1, const OutView* o2,
+                                     const Work& wk, const TileWork& tw, uint32_t n_cu, hipStream_t stream) {
+    static int per_cu = 0;  // resident workgroups per CU (occupancy query, once per shape)
+    if (per_cu == 0) {
+        int nb = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, join_tile_kernel<NT, IPT, true>, NT, 0) != hipSuccess ||
+            nb < 1)
+            nb = 1;
+        per_cu = nb;
+    }
+    const dim3 grid(n_cu * per_cu);
+    if (o2)
+        hipLaunchKernelGGL((join_tile_kernel<NT, IPT, true>), grid, dim3(NT), 0, stream, A, B, o1, *o2, tw, wk);
+    else
+        hipLaunchKernelGGL((join_tile_kernel<NT, IPT, false>), grid, dim3(NT), 0, stream, A, B, o1, o1, tw, wk);
+    return hipGetLastError();
+}
+
+uint32_t tile_positions(uint32_t shape) {
+    switch (shape) {
+        case 1: return 256 * 4;
+        case 2: return 256 * 8;
+        case 3: return 1024 * 2;
+        default: return 512 * 4;
+    }
 }
 
 // Launch the tile path for the worklist the wave kernel filled.  n_cu sizes the
@@ -372,13 +471,12 @@ hipError_t launch_join_tiles(const BatchView& A, const BatchView& B, const OutVi
     hipLaunchKernelGGL((tile_split_kernel<256>), dim3(n_cu * 4), dim3(256), 0, stream, A, B, wk, tw);
     e = hipGetLastError();
     if (e != hipSuccess) return e;
-    if (o2)
-        hipLaunchKernelGGL((join_tile_kernel<kTileNT, kTileIPT, true>), dim3(n_cu * 3), dim3(kTileNT), 0, stream, A,
-                           B, o1, *o2, tw, wk);
-    else
-        hipLaunchKernelGGL((join_tile_kernel<kTileNT, kTileIPT, false>), dim3(n_cu * 3), dim3(kTileNT), 0, stream,
-                           A, B, o1, o1, tw, wk);
-    return hipGetLastError();
+    switch (tw.shape) {
+        case 1: return launch_tile_kernel<256, 4>(A, B, o1, o2, wk, tw, n_cu, stream);
+        case 2: return launch_tile_kernel<256, 8>(A, B, o1, o2, wk, tw, n_cu, stream);
+        case 3: return launch_tile_kernel<1024, 2>(A, B, o1, o2, wk, tw, n_cu, stream);
+        default: return launch_tile_kernel<512, 4>(A, B, o1, o2, wk, tw, n_cu, stream);
+    }
 }
 
 }  // namespace crdt

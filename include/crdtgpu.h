@@ -18,6 +18,10 @@
  *   crdt_causal_context_async
  *       the elementwise max over many version vectors (no reference
  *       counterpart: the per-GPU summary reduced across GPUs by RCCL)
+ *   crdt_awset_apply_async / crdt_awset_apply_batch
+ *       replace the state producers (*AWSet).Add / Del  awset.go:89-101
+ *       and (*AWSetDelta).Del                          awset-delta_test.go:14-33
+ *       applied as ordered op lists to a batch of documents
  *   crdt_global_context_allreduce / crdt_context_allreduce_async
  *       that summary combined across GPUs: RCCL all-reduce(max, u64)
  *       (the reference's counterpart is the CPU max over
@@ -199,6 +203,99 @@ int crdt_gen_zipf_async(crdt_ctx* ctx, uint64_t seed, uint32_t n_docs, const uin
                         const crdt_awset_out* a, const crdt_awset_out* b, void* stream);
 int crdt_gen_replicas_async(crdt_ctx* ctx, uint64_t seed, uint32_t n_docs, uint32_t replicas, uint32_t entries,
                             const crdt_awset_out* dst, const crdt_src_batch* srcs, void* stream);
+
+/* ---- batched local operations: the state producers -----
+ * Each document receives an ordered op list, applied to its replica state
+ * (AWSet entries + VV, and for AWSetDelta its Deleted tombstones) as the
+ * reference's calls would be, in order:
+ *   CRDT_OP_ADD            (*AWSet).Add(k)            awset.go:89-94
+ *                          vv[actor]++; entries[k] = {actor, vv[actor]}
+ *   CRDT_OP_DEL            (*AWSet).Del(k)            awset.go:96-101
+ *                          delete(entries, k); no clock bump
+ *   CRDT_OP_DELTA_DEL      starts one (*AWSetDelta).Del(k...) call,
+ *                          awset-delta_test.go:14-33: vv[actor]++ once
+ *   CRDT_OP_DELTA_DEL_KEY  one key of that call (must follow the
+ *                          DELTA_DEL or another DELTA_DEL_KEY): if k is in
+ *                          entries, Deleted[k] = {actor, vv[actor]} and the
+ *                          entry is deleted; otherwise nothing
+ * Add(k1, k2) / Del(k1, k2) are one op per key in order.  `keys` of
+ * CRDT_OP_DELTA_DEL ops are ignored.  The doc's replica actor is doc_actor[d];
+ * an op that bumps the clock with actor >= R is Go's index-out-of-range panic:
+ * CRDT_E_ACTOR_RANGE.  At most CRDT_MAX_OPS_PER_DOC ops per doc per call
+ * (longer lists: successive calls); malformed lists: CRDT_E_INVALID.
+ * Outputs: doc d's entries at out offset state.offsets[d] + op_off[d]
+ * (capacity = state slots + ops), its tombstones at tombs.offsets[d] +
+ * op_off[d] (tombs NULL: no Deleted yet, offsets 0); tomb_out may be NULL when
+ * no DELTA_DEL_KEY op occurs.  Offsets/counts are written for every doc. */
+#define CRDT_OP_ADD 0
+#define CRDT_OP_DEL 1
+#define CRDT_OP_DELTA_DEL 2
+#define CRDT_OP_DELTA_DEL_KEY 3
+#define CRDT_MAX_OPS_PER_DOC 256
+
+typedef struct {
+    uint32_t n_docs;
+    const uint32_t* op_off;    /* [n_docs+1]  */
+    const uint8_t* kind;       /* [n_ops]     */
+    const uint64_t* keys;      /* [n_ops]     */
+    const uint32_t* doc_actor; /* [n_docs]  AWSet.Actor of each doc's replica */
+} crdt_op_batch;
+
+/* AWSetDelta.Deleted of each doc of a batch (sorted by key). */
+typedef struct {
+    const uint32_t* offsets;  /* [n_docs+1] */
+    const uint32_t* counts;   /* [n_docs] or NULL */
+    const uint64_t* keys;
+    const uint32_t* actors;
+    const uint64_t* counters;
+} crdt_tomb_batch;
+
+typedef struct {
+    uint32_t* offsets;  /* [n_docs+1] */
+    uint32_t* counts;   /* [n_docs]   */
+    uint64_t* keys;
+    uint32_t* actors;
+    uint64_t* counters;
+} crdt_tomb_out;
+
+int crdt_awset_apply_async(crdt_ctx* ctx, const crdt_awset_batch* state, const crdt_tomb_batch* tombs,
+                           const crdt_op_batch* ops, const crdt_awset_out* out, const crdt_tomb_out* tomb_out,
+                           void* stream);
+int crdt_awset_apply_batch(crdt_ctx* ctx, const crdt_awset_batch* state, const crdt_tomb_batch* tombs,
+                           const crdt_op_batch* ops, const crdt_awset_out* out, const crdt_tomb_out* tomb_out);
+
+/* ---- opt-in tombstone GC -------------------------------
+ * The reference never collects tombstones: (*AWSetDelta).gcDeleted is an
+ * empty stub (awset-delta_test.go:67-77) whose comment states the intent,
+ * "remove entries in s.Deleted for srcVersionVector".  Nothing calls this
+ * implicitly.  Doc d keeps tombstone (k, x) unless stable[d*R..].HasDot(x)
+ * (crdt-misc.go:28-34; actor >= R is "not covered", kept).  Pass per doc the
+ * clock every replica has reached (the elementwise min of the replicas' VVs,
+ * crdt_vv_min_async) so that no replica can still need the delete, or the
+ * source VV of the last merge for the stub's literal reading.  Output at the
+ * input's slot offsets, compacted, in key order. */
+int crdt_tombstone_gc_async(crdt_ctx* ctx, const crdt_tomb_batch* tombs, uint32_t n_docs, uint32_t R,
+                            const uint64_t* stable_vv, const crdt_tomb_out* out, void* stream);
+/* dst[i] = min(dst[i], src[i]) for i < n (u64): causal stability across replicas. */
+int crdt_vv_min_async(crdt_ctx* ctx, uint64_t* dst, const uint64_t* src, size_t n, void* stream);
+
+/* ---- fixture dumps and debug text, host buffers -------
+ * crdt_awset_format: Go's (AWSet).String() of doc `doc` (awset.go:163-171:
+ * VersionVector.String crdt-misc.go:57-68, then "
+  %s  %q" per entry in
+ * sorted key order, Dot.String crdt-misc.go:17-19).  names[id] is the string
+ * of key id (ids order-preserving); names == NULL prints "#<id>".  The VV
+ * prints all R words.  Writes at most cap bytes including the NUL; *len = the
+ * full length.
+ * crdt_batch_dump: a self-checking binary image of a batch (live entries
+ * only, compact offsets); buf == NULL: *len = the size needed.
+ * crdt_batch_info / crdt_batch_undump: check an image and read its sizes, then
+ * fill caller arrays (offsets n_docs+1, counts, n_entries entries, n_docs*R vv). */
+int crdt_awset_format(const crdt_awset_batch* b, uint32_t doc, const char* const* names, char* buf, size_t cap,
+                      size_t* len);
+int crdt_batch_dump(const crdt_awset_batch* b, void* buf, size_t cap, size_t* len);
+int crdt_batch_info(const void* buf, size_t len, uint32_t* n_docs, uint32_t* R, uint64_t* n_entries);
+int crdt_batch_undump(const void* buf, size_t len, const crdt_awset_out* out);
 
 /* ---- multi-GPU: the global causal context over RCCL (xGMI) --------------
  * Documents shard over GPUs with no exchange; the one collective is the

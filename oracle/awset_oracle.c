@@ -348,3 +348,164 @@ void oracle_causal_context(const uint64_t* vv, uint32_t n_docs, uint32_t R, uint
     for (uint32_t r = 0; r < R; r++) out[r] = 0;
     for (uint32_t d = 0; d < n_docs; d++) vv_merge(out, vv + (size_t)d * R, R);
 }
+
+/* ---- batched local ops: the state producers, op by op ------------------- */
+
+/* sorted-array map: set e[key] = v (insert or overwrite); cap must allow n+1 */
+static void map_set(ent* e, size_t* n, ent v) {
+    size_t lo = 0, hi = *n;
+    while (lo < hi) {
+        size_t mid = lo + (hi - lo) / 2;
+        if (e[mid].key < v.key)
+            lo = mid + 1;
+        else
+            hi = mid;
+    }
+    if (lo < *n && e[lo].key == v.key) {
+        e[lo] = v;
+        return;
+    }
+    memmove(e + lo + 1, e + lo, (*n - lo) * sizeof(ent));
+    e[lo] = v;
+    (*n)++;
+}
+
+/* delete(e, key) */
+static void map_del(ent* e, size_t* n, uint64_t key) {
+    long i = find(e, *n, key);
+    if (i < 0) return;
+    memmove(e + i, e + i + 1, (*n - (size_t)i - 1) * sizeof(ent));
+    (*n)--;
+}
+
+/*
+ * Each doc's ops, in order, on its replica state (entries, VV, Deleted):
+ *   CRDT_OP_ADD            awset.go:89-94   vv[actor]++; entries[k] = {actor, vv[actor]}
+ *   CRDT_OP_DEL            awset.go:96-101  delete(entries, k)
+ *   CRDT_OP_DELTA_DEL      awset-delta_test.go:14-16  vv[actor]++; dot2 = {actor, vv[actor]}
+ *   CRDT_OP_DELTA_DEL_KEY  awset-delta_test.go:17-31  if k in entries: Deleted[k] = dot2, delete
+ * VersionVector[actor]++ with actor >= len(vv) is Go's index panic:
+ * CRDT_E_ACTOR_RANGE.  The device limit of CRDT_MAX_OPS_PER_DOC ops per doc
+ * and the DELTA_DEL_KEY placement rule are checked too (CRDT_E_INVALID).
+ */
+int oracle_awset_apply(const crdt_awset_batch* st, const crdt_tomb_batch* tb, const crdt_op_batch* ops,
+                       const crdt_awset_out* out, const crdt_tomb_out* tout) {
+    const uint32_t R = st->R, n = st->n_docs;
+    int rc = 0;
+    size_t cap = 1;
+    for (uint32_t d = 0; d < n; d++) {
+        size_t c = (size_t)(st->offsets[d + 1] - st->offsets[d]) + (tb ? tb->offsets[d + 1] - tb->offsets[d] : 0) +
+                   (ops->op_off[d + 1] - ops->op_off[d]) + 1;
+        if (c > cap) cap = c;
+    }
+    ent* e = (ent*)malloc(cap * sizeof(ent));
+    ent* t = (ent*)malloc(cap * sizeof(ent));
+    uint64_t* vv = (uint64_t*)malloc((R ? R : 1) * sizeof(uint64_t));
+    if (!e || !t || !vv) {
+        free(e);
+        free(t);
+        free(vv);
+        return CRDT_E_NOMEM;
+    }
+    for (uint32_t d = 0; d < n && !rc; d++) {
+        const uint32_t so = st->offsets[d];
+        size_t ne = st->counts ? st->counts[d] : st->offsets[d + 1] - so;
+        gather(e, st->keys, st->actors, st->counters, so, so + (uint32_t)ne);
+        size_t nt = 0;
+        uint32_t to = 0;
+        if (tb) {
+            to = tb->offsets[d];
+            nt = tb->counts ? tb->counts[d] : tb->offsets[d + 1] - to;
+            gather(t, tb->keys, tb->actors, tb->counters, to, to + (uint32_t)nt);
+        }
+        memcpy(vv, st->vv + (size_t)d * R, R * sizeof(uint64_t));
+        const uint32_t o0 = ops->op_off[d], no = ops->op_off[d + 1] - o0;
+        const uint32_t actor = ops->doc_actor[d];
+        if (no > CRDT_MAX_OPS_PER_DOC) rc = CRDT_E_INVALID;
+        uint64_t dot2 = 0;
+        for (uint32_t j = 0; j < no && !rc; j++) {
+            const uint32_t kind = ops->kind[o0 + j];
+            const uint64_t key = ops->keys[o0 + j];
+            const uint32_t prev = j ? ops->kind[o0 + j - 1] : 0xFFu;
+            if (kind == CRDT_OP_ADD || kind == CRDT_OP_DELTA_DEL) {
+                if (actor >= R) {
+                    rc = CRDT_E_ACTOR_RANGE;
+                    break;
+                }
+                vv[actor]++;
+            }
+            if (kind == CRDT_OP_ADD) {
+                ent v = {key, actor, vv[actor]};
+                map_set(e, &ne, v);
+            } else if (kind == CRDT_OP_DEL) {
+                map_del(e, &ne, key);
+            } else if (kind == CRDT_OP_DELTA_DEL) {
+                dot2 = vv[actor];
+            } else if (kind == CRDT_OP_DELTA_DEL_KEY) {
+                if ((prev != CRDT_OP_DELTA_DEL && prev != CRDT_OP_DELTA_DEL_KEY) || !tout) {
+                    rc = CRDT_E_INVALID;
+                    break;
+                }
+                if (find(e, ne, key) >= 0) {
+                    ent v = {key, actor, dot2};
+                    map_set(t, &nt, v);
+                    map_del(e, &ne, key);
+                }
+            } else {
+                rc = CRDT_E_INVALID;
+            }
+        }
+        if (rc) break;
+        const uint32_t base = so + o0;
+        out->offsets[d] = base;
+        out->counts[d] = (uint32_t)ne;
+        for (size_t i = 0; i < ne; i++) {
+            out->keys[base + i] = e[i].key;
+            out->actors[base + i] = e[i].actor;
+            out->counters[base + i] = e[i].counter;
+        }
+        memcpy(out->vv + (size_t)d * R, vv, R * sizeof(uint64_t));
+        if (tout) {
+            const uint32_t tbase = to + o0;
+            tout->offsets[d] = tbase;
+            tout->counts[d] = (uint32_t)nt;
+            for (size_t i = 0; i < nt; i++) {
+                tout->keys[tbase + i] = t[i].key;
+                tout->actors[tbase + i] = t[i].actor;
+                tout->counters[tbase + i] = t[i].counter;
+            }
+        }
+    }
+    if (!rc) {
+        out->offsets[n] = st->offsets[n] + ops->op_off[n];
+        if (tout) tout->offsets[n] = (tb ? tb->offsets[n] : 0) + ops->op_off[n];
+    }
+    free(e);
+    free(t);
+    free(vv);
+    return rc;
+}
+
+/* Opt-in tombstone GC (no reference counterpart: gcDeleted is empty,
+ * awset-delta_test.go:67-77): keep (k, x) unless stable.HasDot(x), with
+ * actor >= R kept.  Same layout as crdt_tombstone_gc_async. */
+int oracle_tomb_gc(const crdt_tomb_batch* tb, uint32_t n_docs, uint32_t R, const uint64_t* stable,
+                   const crdt_tomb_out* out) {
+    for (uint32_t d = 0; d < n_docs; d++) {
+        const uint32_t o = tb->offsets[d];
+        const uint32_t n = tb->counts ? tb->counts[d] : tb->offsets[d + 1] - o;
+        uint32_t k = 0;
+        for (uint32_t i = 0; i < n; i++) {
+            const uint32_t a = tb->actors[o + i];
+            if (a < R && stable[(size_t)d * R + a] >= tb->counters[o + i]) continue;
+            out->keys[o + k] = tb->keys[o + i];
+            out->actors[o + k] = a;
+            out->counters[o + k] = tb->counters[o + i];
+            k++;
+        }
+        out->offsets[d] = o;
+        out->counts[d] = k;
+    }
+    out->offsets[n_docs] = tb->offsets[n_docs];
+    return 0;
+}

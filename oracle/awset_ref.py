@@ -85,6 +85,57 @@ class VersionVector(list):
         return "[" + ", ".join("(%s %d)" % (chr(ord("A") + i), n) for i, n in enumerate(self)) + "]"
 
 
+def _go_printable(r: int) -> bool:
+    # unicode.IsPrint, exact for ASCII; outside ASCII the same approximation as
+    # csrc/serial.cpp (controls, format characters, separators, private use and
+    # non-characters are not printable)
+    if r < 0x20 or r == 0x7F:
+        return False
+    if r < 0x7F:
+        return True
+    if 0x80 <= r <= 0xA0 or r == 0xAD or 0x2000 <= r <= 0x200F or 0x2028 <= r <= 0x202F:
+        return False
+    if 0x205F <= r <= 0x206F or r in (0x3000, 0xFEFF) or 0xE000 <= r <= 0xF8FF:
+        return False
+    if (r & 0xFFFE) == 0xFFFE or 0xFDD0 <= r <= 0xFDEF or r >= 0xF0000:
+        return False
+    return True
+
+
+def go_quote(s) -> str:
+    """fmt %q of a Go string (strconv.Quote); s is str or bytes (bytes may hold
+    invalid UTF-8, escaped as \\xNN)."""
+    b = s.encode("utf-8", errors="surrogateescape") if isinstance(s, str) else bytes(s)
+    out, i = ['"'], 0
+    esc = {7: "\\a", 8: "\\b", 12: "\\f", 10: "\\n", 13: "\\r", 9: "\\t", 11: "\\v"}
+    while i < len(b):
+        c = b[i]
+        n = 1 if c < 0x80 else 2 if c >> 5 == 6 else 3 if c >> 4 == 14 else 4 if c >> 3 == 30 else 0
+        try:
+            r = ord(b[i:i + n].decode("utf-8")) if n else None
+        except UnicodeDecodeError:
+            r = None
+        if r is None:
+            out.append("\\x%02x" % c)
+            i += 1
+            continue
+        if r in (0x22, 0x5C):
+            out.append("\\" + chr(r))
+        elif _go_printable(r):
+            out.append(chr(r))
+        elif r in esc:
+            out.append(esc[r])
+        elif r < 0x20 or r == 0x7F:
+            out.append("\\x%02x" % r)
+        elif r < 0x10000:
+            out.append("\\u%04x" % r)
+        else:
+            out.append("\\U%08x" % r)
+        i += n
+    out.append('"')
+    return "".join(out)
+
+
 class AWSet:
     """awset.go:55-59 -- ``{Actor, VersionVector, Entries map[string]Dot}``."""
 
@@ -158,10 +209,10 @@ class AWSet:
             # absent: delete of a missing key is a no-op (:160-163)
         dst.VersionVector.Merge(srcVV)  # :165
 
-    def String(self) -> str:  # awset.go:163-171
+    def String(self) -> str:  # awset.go:163-171: "\n  %s  %q" per value
         out = self.VersionVector.String()
         for v in self.SortedValues():
-            out += '\n  %s  "%s"' % (self.Entries[v], v)
+            out += "\n  %s  %s" % (self.Entries[v], go_quote(v))
         return out
 
 

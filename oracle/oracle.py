@@ -19,8 +19,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 sys.path.insert(0, os.path.join(ROOT, "go-crdt-playground_amd"))
 
-from crdtgpu.abi import CAWSetBatch, CAWSetOut, CSrcBatch  # noqa: E402
-from crdtgpu.batch import AWSetBatch, OutBuffers, SrcBatch  # noqa: E402
+from crdtgpu.abi import CAWSetBatch, CAWSetOut, COpBatch, CSrcBatch, CTombBatch, CTombOut  # noqa: E402
+from crdtgpu.batch import AWSetBatch, OpBatch, OutBuffers, SrcBatch, TombBatch, TombBuffers  # noqa: E402
 
 LIB = os.path.join(HERE, "build", "liboracle.so")
 MAPLIB = os.path.join(HERE, "build", "libawsetmap.so")
@@ -45,6 +45,10 @@ def lib():
         _lib.oracle_awset_join.argtypes = [P(CAWSetBatch), P(CAWSetBatch), P(CAWSetOut)]
         _lib.oracle_awset_fold.restype = ctypes.c_int
         _lib.oracle_awset_fold.argtypes = [ctypes.c_int, P(CAWSetBatch), P(CSrcBatch), P(CAWSetOut)]
+        _lib.oracle_awset_apply.restype = ctypes.c_int
+        _lib.oracle_awset_apply.argtypes = [P(CAWSetBatch), P(CTombBatch), P(COpBatch), P(CAWSetOut), P(CTombOut)]
+        _lib.oracle_tomb_gc.restype = ctypes.c_int
+        _lib.oracle_tomb_gc.argtypes = [P(CTombBatch), ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p, P(CTombOut)]
         _lib.oracle_causal_context.restype = None
         _lib.oracle_causal_context.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p]
     return _lib
@@ -64,6 +68,33 @@ def fold(mode: int, dst: AWSetBatch, srcs: SrcBatch):
     out = OutBuffers(dst.n_docs, dst.R, srcs.out_slots(dst))
     d, s, o = dst.c(), srcs.c(), out.c()
     rc = lib().oracle_awset_fold(int(mode), ctypes.byref(d), ctypes.byref(s), ctypes.byref(o))
+    return rc, out
+
+
+def apply(state: AWSetBatch, ops: OpBatch, tombs: TombBatch = None, with_tombs: bool = True):
+    """(status, entries out, tombstones out or None) after each doc's local ops
+    (awset.go:89-101, awset-delta_test.go:14-33), same layout as crdt_awset_apply_*."""
+    state, ops = state.numpy(), ops.numpy()
+    tombs = tombs.numpy() if tombs is not None else None
+    nops = int(ops.op_off[-1])
+    out = OutBuffers(state.n_docs, state.R, int(state.offsets[-1]) + nops)
+    tout = TombBuffers(state.n_docs, (int(tombs.offsets[-1]) if tombs is not None else 0) + nops) if with_tombs else None
+    cs, co, cout = state.c(), ops.c(), out.c()
+    ct = tombs.c() if tombs is not None else None
+    cto = tout.c_out() if tout is not None else None
+    rc = lib().oracle_awset_apply(ctypes.byref(cs), ctypes.byref(ct) if ct else None, ctypes.byref(co),
+                                  ctypes.byref(cout), ctypes.byref(cto) if cto else None)
+    return rc, out, tout
+
+
+def tomb_gc(tombs: TombBatch, R: int, stable: np.ndarray):
+    """(status, TombBuffers): tombstones not covered by each doc's stable clock."""
+    tombs = tombs.numpy()
+    n = tombs.n_docs
+    out = TombBuffers(n, int(tombs.offsets[-1]))
+    st = np.ascontiguousarray(stable, dtype=np.uint64)
+    ct, co = tombs.c(), out.c_out()
+    rc = lib().oracle_tomb_gc(ctypes.byref(ct), n, int(R), st.ctypes.data, ctypes.byref(co))
     return rc, out
 
 

@@ -1,0 +1,53 @@
+#!/usr/bin/env python3
+"""Sweep the large-document tile kernel's shape (crdt_ctx_set_option
+"join_tile_shape") on the config-4 exchange: HIP-event time per call.
+GPU box only."""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "go-crdt-playground_amd")]
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import crdtgpu  # noqa: E402
+from crdtgpu.batch import OutBuffers  # noqa: E402
+from crdtgpu.engine import zipf_sizes  # noqa: E402
+
+
+def main():
+    n = int(sys.argv[1]) if len(sys.argv) > 1 else 16384
+    dev = torch.device("cuda:0")
+    eng = crdtgpu.Engine(0)
+    sizes = zipf_sizes(0x5EED, n)
+    offs = np.zeros(n + 1, dtype=np.uint32)
+    np.cumsum(sizes, out=offs[1:])
+    total = int(offs[-1])
+    d_offs = torch.from_numpy(offs.view(np.int32).copy()).to(dev)
+    A, B = OutBuffers(n, 2, total, device=dev), OutBuffers(n, 2, total, device=dev)
+    eng.gen_zipf_async(0x5EED, n, d_offs, A, B)
+    o1, o2 = OutBuffers(n, 2, 2 * total, device=dev), OutBuffers(n, 2, 2 * total, device=dev)
+    a, b = A.as_batch(), B.as_batch()
+    ref = None
+    for shape in (0, 1, 2, 3, 0):
+        eng.set_option("join_tile_shape", shape)
+        eng.exchange_async(a, b, o1, o2)
+        eng.sync()
+        got = (o1.counts.clone(), o1.keys[:: 9973].clone(), o2.counters[:: 9973].clone())
+        if ref is None:
+            ref = got
+        same = all(torch.equal(x, y) for x, y in zip(ref, got))
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+        ev[0].record()
+        for _ in range(5):
+            eng.exchange_async(a, b, o1, o2)
+        ev[1].record()
+        eng.sync()
+        print("shape %d: %.3f ms per exchange call (same output: %s)" % (shape, ev[0].elapsed_time(ev[1]) / 5, same),
+              flush=True)
+    eng.close()
+
+
+if __name__ == "__main__":
+    main()
