@@ -17,9 +17,12 @@ local ops (Add, Del, Clone, ...) are per-replica host state changes, as in the
 reference; they are not part of the batched hot path.
 
 Differences from the Go code, all at inputs where Go panics or is ambiguous:
-  * a batch's version vectors are zero-padded to the longest one (R <= 64);
-    ``HasDot`` at actor == len(vv) of a shorter vector then reads the pad
-    instead of panicking.  Equal-length vectors (every reference test) are exact.
+  * a batch's version vectors are zero-padded to the longest one (R <= 64).
+    The kernels flag HasDot at actor == R; for a shorter vector the panic at
+    actor == len(vv) is found on the host before the launch -- exactly for
+    MergeBatch (the HasDot calls of awset.go:133 and :152 are replayed on the
+    keys alone).  Folds over vectors of unequal lengths read the pad instead
+    of panicking; equal-length vectors (every reference test) are exact.
   * where Go panics (actor == len(vv)), the merge raises CrdtError
     (CRDT_E_ACTOR_RANGE) and leaves the destination untouched.
 """
@@ -202,6 +205,16 @@ def _unpack(dsts, out, names, R, widths):
         dst.VersionVector = VersionVector(out.vv[d * R:d * R + widths[d]].tolist())
 
 
+def _join_panics(dst: "AWSet", src: "AWSet") -> bool:
+    """Would dst.Merge(src) panic in Go at a HasDot with actor == len(vv)?  The
+    reference evaluates dstVV.HasDot(s) for every src-only key (awset.go:133)
+    and srcVV.HasDot(d) for every dst-only key (:152)."""
+    ld, ls = len(dst.VersionVector), len(src.VersionVector)
+    if any(k not in dst.Entries and s.Actor == ld for k, s in src.Entries.items()):
+        return True
+    return any(k not in src.Entries and d.Actor == ls for k, d in dst.Entries.items())
+
+
 def MergeBatch(dsts: Sequence[AWSet], srcs: Sequence[AWSet], engine: Optional[Engine] = None) -> None:
     """dsts[i].Merge(srcs[i]) for every i, as one batched GPU join (dsts must be distinct)."""
     if len(dsts) != len(srcs):
@@ -209,9 +222,12 @@ def MergeBatch(dsts: Sequence[AWSet], srcs: Sequence[AWSet], engine: Optional[En
     if not dsts:
         return
     states = list(dsts) + list(srcs)
+    R = _width(states)
+    for a, b in zip(dsts, srcs):  # vectors shorter than R: their panic point is below the kernels' actor == R
+        if (len(a.VersionVector) < R or len(b.VersionVector) < R) and _join_panics(a, b):
+            raise abi.CrdtError(abi.CRDT_E_ACTOR_RANGE, "MergeBatch: HasDot at actor == len(vv)")
     ids = _intern(states)
     names = {i: k for k, i in ids.items()}
-    R = _width(states)
     db = AWSetBatch.from_docs(R, [(_entries(s.Entries, ids), _pad(s.VersionVector, R)) for s in dsts])
     sb = AWSetBatch.from_docs(R, [(_entries(s.Entries, ids), _pad(s.VersionVector, R)) for s in srcs])
     out = (engine or default_engine()).join(db, sb)

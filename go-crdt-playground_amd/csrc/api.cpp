@@ -104,7 +104,8 @@ struct crdt_ctx {
     DevBuf tile_desc, tile_flags, tile_slot, tile_run;
     uint32_t tile_cap = 1u << 20;             // crdt_ctx_set_option("join_tile_capacity")
     bool join_tiles = true;                   // crdt_ctx_set_option("join_tiles")
-    uint32_t tile_shape = 0;                  // crdt_ctx_set_option("join_tile_shape")
+    uint32_t tile_shape = 2;                  // crdt_ctx_set_option("join_tile_shape")
+    bool tile_nt_stores = true;               // crdt_ctx_set_option("join_tile_nt_stores")
     size_t scratch_slots = 0;
     uint32_t max_doc_entries = 0xFFFFFFFFu;  // caller's promise (crdt_ctx_set_max_doc_entries)
     uint32_t join_docs_per_wave = 8;          // crdt_ctx_set_option("join_docs_per_wave")
@@ -315,9 +316,13 @@ int crdt_ctx_set_option(crdt_ctx* ctx, const char* name, int64_t value) {
         ctx->tile_cap = (uint32_t)value;
         return CRDT_OK;
     }
-    if (!strcmp(name, "join_tile_shape")) {  // 0: 512x4, 1: 256x4, 2: 256x8, 3: 1024x2 (threads x positions)
+    if (!strcmp(name, "join_tile_shape")) {  // 0: 512x4, 1: 256x4, 2: 256x8 (default), 3: 1024x2 (threads x positions)
         if (value < 0 || value > 3) return CRDT_E_INVALID;
         ctx->tile_shape = (uint32_t)value;
+        return CRDT_OK;
+    }
+    if (!strcmp(name, "join_tile_nt_stores")) {
+        ctx->tile_nt_stores = value != 0;
         return CRDT_OK;
     }
     if (!strcmp(name, "join_tiles")) {  // 0: large documents one workgroup each (join_block_kernel)
@@ -377,7 +382,7 @@ static int join_common(crdt_ctx* ctx, const crdt_awset_batch* dst, const crdt_aw
         uint32_t* w = ctx->ws.as<uint32_t>(0);
         tw = TileWork{ctx->tile_desc.as<uint4>(), ctx->tile_flags.as<uint64_t>(), ctx->tile_slot.as<uint32_t>(),
                       ctx->tile_run.as<uint32_t>(), w + 3, w + 4, w + 5, ctx->tile_cap,
-                      tile_positions(ctx->tile_shape), ctx->tile_shape};
+                      tile_positions(ctx->tile_shape), ctx->tile_shape, ctx->tile_nt_stores ? 1u : 0u};
     }
     // the per-call counters are read only by the large-document paths
     if (!no_large && launch_reset_work(ctx->ws.as<uint32_t>(0), s) != hipSuccess) return CRDT_E_HIP;

@@ -109,6 +109,7 @@ struct TileWork {
     uint32_t cap;
     uint32_t tile;   // merged positions per tile (= the tile kernel's NT * IPT)
     uint32_t shape;  // tile kernel shape (tile.hip, tile_positions)
+    uint32_t nt_stores;  // non-temporal output stores ("join_tile_nt_stores")
 };
 
 __device__ __forceinline__ uint32_t live_count(const uint32_t* offsets, const uint32_t* counts, uint32_t d) {

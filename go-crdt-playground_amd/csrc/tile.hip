@@ -266,7 +266,15 @@ __device__ __forceinline__ void tile_issue(const BatchView& A, const BatchView& 
 // of this tile waits on another workgroup, so a taken tile is never held
 // behind a wait), and its loads are issued before this tile's output stores,
 // which they overlap.
-template <int NT, int IPT, bool EXCH>
+template <typename T, bool NTS>
+__device__ __forceinline__ void out_store(T v, T* p) {
+    if (NTS)
+        __builtin_nontemporal_store(v, p);
+    else
+        *p = v;
+}
+
+template <int NT, int IPT, bool EXCH, bool NTS>
 __global__ __launch_bounds__(NT) void join_tile_kernel(BatchView A, BatchView B, OutView o1, OutView o2,
                                                        TileWork tw, Work wk) {
     __shared__ TileSmem<NT, IPT> sm;
@@ -402,13 +410,13 @@ __global__ __launch_bounds__(NT) void join_tile_kernel(BatchView A, BatchView B,
                     const uint32_t v = sm.stage[p];
                     const uint32_t x1 = v & 0xFFFFu, x2 = v >> 16;
                     const uint64_t key = sm.key[x1];
-                    __builtin_nontemporal_store(key, o1.keys + obase + p);
-                    __builtin_nontemporal_store(sm.act[x1], o1.actors + obase + p);
-                    __builtin_nontemporal_store(sm.ctr[x1], o1.counters + obase + p);
+                    out_store<uint64_t, NTS>(key, o1.keys + obase + p);
+                    out_store<uint32_t, NTS>(sm.act[x1], o1.actors + obase + p);
+                    out_store<uint64_t, NTS>(sm.ctr[x1], o1.counters + obase + p);
                     if (EXCH) {
-                        __builtin_nontemporal_store(key, o2.keys + obase + p);
-                        __builtin_nontemporal_store(sm.act[x2], o2.actors + obase + p);
-                        __builtin_nontemporal_store(sm.ctr[x2], o2.counters + obase + p);
+                        out_store<uint64_t, NTS>(key, o2.keys + obase + p);
+                        out_store<uint32_t, NTS>(sm.act[x2], o2.actors + obase + p);
+                        out_store<uint64_t, NTS>(sm.ctr[x2], o2.counters + obase + p);
                     }
                 }
             }
@@ -429,23 +437,31 @@ __global__ __launch_bounds__(NT) void join_tile_kernel(BatchView A, BatchView B,
 }
 
 // Tile shapes (workgroup size x positions per thread); "join_tile_shape".
-template <int NT, int IPT>
-static hipError_t launch_tile_kernel(const BatchView& A, const BatchView& B, const OutView& o1, const OutView* o2,
-                                     const Work& wk, const TileWork& tw, uint32_t n_cu, hipStream_t stream) {
+template <int NT, int IPT, bool NTS>
+static hipError_t launch_tile_kernel_s(const BatchView& A, const BatchView& B, const OutView& o1, const OutView* o2,
+                                       const Work& wk, const TileWork& tw, uint32_t n_cu, hipStream_t stream) {
     static int per_cu = 0;  // resident workgroups per CU (occupancy query, once per shape)
     if (per_cu == 0) {
         int nb = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, join_tile_kernel<NT, IPT, true>, NT, 0) != hipSuccess ||
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, join_tile_kernel<NT, IPT, true, NTS>, NT, 0) !=
+                hipSuccess ||
             nb < 1)
             nb = 1;
         per_cu = nb;
     }
     const dim3 grid(n_cu * per_cu);
     if (o2)
-        hipLaunchKernelGGL((join_tile_kernel<NT, IPT, true>), grid, dim3(NT), 0, stream, A, B, o1, *o2, tw, wk);
+        hipLaunchKernelGGL((join_tile_kernel<NT, IPT, true, NTS>), grid, dim3(NT), 0, stream, A, B, o1, *o2, tw, wk);
     else
-        hipLaunchKernelGGL((join_tile_kernel<NT, IPT, false>), grid, dim3(NT), 0, stream, A, B, o1, o1, tw, wk);
+        hipLaunchKernelGGL((join_tile_kernel<NT, IPT, false, NTS>), grid, dim3(NT), 0, stream, A, B, o1, o1, tw, wk);
     return hipGetLastError();
+}
+
+template <int NT, int IPT>
+static hipError_t launch_tile_kernel(const BatchView& A, const BatchView& B, const OutView& o1, const OutView* o2,
+                                     const Work& wk, const TileWork& tw, uint32_t n_cu, hipStream_t stream) {
+    return tw.nt_stores ? launch_tile_kernel_s<NT, IPT, true>(A, B, o1, o2, wk, tw, n_cu, stream)
+                        : launch_tile_kernel_s<NT, IPT, false>(A, B, o1, o2, wk, tw, n_cu, stream);
 }
 
 uint32_t tile_positions(uint32_t shape) {

@@ -6,7 +6,8 @@
 //   AWSet                             awset.go:55-171
 //   AWSetDelta                        awset-delta_test.go:9-77
 // Merge() and the batch entry points (MergeBatch, FoldBatch, DeltaMergeBatch)
-// intern the string keys of the batch into order-preserving u64 ids, pack the
+// intern the string keys of each document into order-preserving u64 ids (the
+// ranks of the document's keys; host work spread over threads), pack the
 // structure-of-arrays buffers of include/crdtgpu.h, run the HIP kernels through
 // crdt_awset_join_batch / crdt_awset_fold_batch and unpack the result.  Local
 // ops (Add, Del, Clone, ...) are per-replica host state, as in the reference.
@@ -14,14 +15,18 @@
 // Where the Go code panics (HasDot/Counter at actor == len(vv), Add with the
 // actor outside the vector), this API throws crdt::Error carrying the C ABI
 // code (CRDT_E_ACTOR_RANGE); a failed merge leaves its destinations untouched.
-// Version vectors of one batch are zero-padded to the longest (<= 64).
+// Version vectors of one batch are zero-padded to the longest (<= 64); for a
+// join the panic at actor == len(vv) of a shorter vector is found on the host
+// (detail::join_panics), folds over unequal lengths read the pad.
 #pragma once
 
 #include <algorithm>
 #include <cstdint>
+#include <cstdlib>
 #include <map>
 #include <stdexcept>
 #include <string>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
@@ -181,56 +186,101 @@ struct Packed {
     std::vector<uint64_t> vv;
 };
 
-inline void pack_entries(const Entries& m, const std::map<std::string, uint64_t>& id, std::vector<uint64_t>& k,
-                         std::vector<uint32_t>& a, std::vector<uint64_t>& c) {
-    std::vector<std::pair<uint64_t, Dot>> v;
-    v.reserve(m.size());
-    for (auto& kv : m) v.emplace_back(id.at(kv.first), kv.second);
-    std::sort(v.begin(), v.end(), [](auto& x, auto& y) { return x.first < y.first; });
-    for (auto& e : v) {
-        k.push_back(e.first);
-        a.push_back(e.second.actor);
-        c.push_back(e.second.counter);
-    }
-}
-
-inline void pack_vv(const VersionVector& v, size_t R, std::vector<uint64_t>& out) {
-    for (size_t r = 0; r < R; ++r) out.push_back(r < v.size() ? v[r] : 0);
-}
-
 template <typename T>
 T* data_or_null(std::vector<T>& v) {
     return v.empty() ? nullptr : v.data();
 }
 
-// Interning + packing shared by the batch entry points.
-struct Batch {
-    std::map<std::string, uint64_t> id;
-    std::vector<const std::string*> name;
-    size_t R = 1;
+// Worker threads for the per-document host work (interning, packing,
+// unpacking): CRDT_HOST_THREADS, else OMP_NUM_THREADS, else the hardware
+// threads (at most 16); 1 = serial.
+inline unsigned host_threads() {
+    static const unsigned n = [] {
+        for (const char* name : {"CRDT_HOST_THREADS", "OMP_NUM_THREADS"}) {
+            const char* e = std::getenv(name);
+            const long v = e ? std::strtol(e, nullptr, 10) : 0;
+            if (v > 0) return (unsigned)std::min(v, 256L);
+        }
+        return std::min(std::max(1u, std::thread::hardware_concurrency()), 16u);
+    }();
+    return n;
+}
 
-    void scan(const AWSet& s) {
-        for (auto& kv : s.entries) id.emplace(kv.first, 0);
-        if (auto* d = s.deleted_map())
-            for (auto& kv : *d) id.emplace(kv.first, 0);
-        R = std::max(R, s.versionVector.size());
+template <typename F>
+void parallel_docs(size_t n, F&& fn) {
+    const unsigned t = (unsigned)std::min<size_t>(host_threads(), std::max<size_t>(1, n / 256));
+    if (t <= 1) {
+        fn(0, n);
+        return;
     }
-    void finish() {
-        if (R > CRDT_MAX_R) throw Error(CRDT_E_INVALID, "version vector longer than CRDT_MAX_R");
-        uint64_t i = 0;
-        name.resize(id.size());
-        for (auto& kv : id) {
-            kv.second = i;
-            name[i++] = &kv.first;
+    std::vector<std::thread> pool;
+    const size_t chunk = (n + t - 1) / t;
+    for (unsigned i = 0; i < t; ++i) {
+        const size_t lo = i * chunk, hi = std::min(n, lo + chunk);
+        if (lo < hi) pool.emplace_back([&fn, lo, hi] { fn(lo, hi); });
+    }
+    for (auto& th : pool) th.join();
+}
+
+// Interning + packing shared by the batch entry points.  Keys are interned
+// per document: the merge only ever compares keys of one document, so a
+// document's ids are the ranks of its keys (over every state of that document
+// in the batch) in string order -- an exact, order-preserving bijection per
+// document, as the C ABI requires, built from a small sort per document.
+struct Batch {
+    size_t R = 1;
+    std::vector<std::vector<const std::string*>> names;  // doc -> id -> key
+
+    // doc d's states: every key of each (entries and Deleted) becomes an id
+    void intern(size_t d, const std::vector<const AWSet*>& states) {
+        auto& v = names[d];
+        v.clear();
+        for (auto* s : states) {
+            for (auto& kv : s->entries) v.push_back(&kv.first);
+            if (auto* del = s->deleted_map())
+                for (auto& kv : *del) v.push_back(&kv.first);
+        }
+        std::sort(v.begin(), v.end(), [](const std::string* a, const std::string* b) { return *a < *b; });
+        v.erase(std::unique(v.begin(), v.end(), [](const std::string* a, const std::string* b) { return *a == *b; }),
+                v.end());
+    }
+    uint64_t id(size_t d, const std::string& k) const {
+        const auto& v = names[d];
+        return (uint64_t)(std::lower_bound(v.begin(), v.end(), &k,
+                                           [](const std::string* a, const std::string* b) { return *a < *b; }) -
+                          v.begin());
+    }
+    // write map m of doc d at k/a/c[at..], sorted by id
+    void put_entries(size_t d, const Entries& m, uint64_t* k, uint32_t* a, uint64_t* c) const {
+        std::vector<std::pair<uint64_t, Dot>> v;
+        v.reserve(m.size());
+        for (auto& kv : m) v.emplace_back(id(d, kv.first), kv.second);
+        std::sort(v.begin(), v.end(), [](auto& x, auto& y) { return x.first < y.first; });
+        for (size_t i = 0; i < v.size(); ++i) {
+            k[i] = v[i].first;
+            a[i] = v[i].second.actor;
+            c[i] = v[i].second.counter;
         }
     }
+    // one state per doc (states[d] of doc d), offsets = prefix of entry counts
     Packed pack(const std::vector<AWSet*>& states) const {
         Packed p;
-        for (auto* s : states) {
-            pack_entries(s->entries, id, p.keys, p.actors, p.counters);
-            p.offsets.push_back((uint32_t)p.keys.size());
-            pack_vv(s->versionVector, R, p.vv);
-        }
+        const size_t n = states.size();
+        p.offsets.assign(n + 1, 0);
+        for (size_t d = 0; d < n; ++d) p.offsets[d + 1] = p.offsets[d] + (uint32_t)states[d]->entries.size();
+        const size_t tot = p.offsets[n];
+        p.keys.resize(tot);
+        p.actors.resize(tot);
+        p.counters.resize(tot);
+        p.vv.assign(n * R, 0);
+        parallel_docs(n, [&](size_t lo, size_t hi) {
+            for (size_t d = lo; d < hi; ++d) {
+                const uint32_t o = p.offsets[d];
+                put_entries(d, states[d]->entries, p.keys.data() + o, p.actors.data() + o, p.counters.data() + o);
+                const auto& v = states[d]->versionVector;
+                for (size_t r = 0; r < std::min(R, v.size()); ++r) p.vv[d * R + r] = v[r];
+            }
+        });
         return p;
     }
     crdt_awset_batch view(Packed& p) const {
@@ -240,16 +290,18 @@ struct Batch {
     }
     void unpack(const std::vector<AWSet*>& dsts, const Packed& out, const std::vector<uint32_t>& counts,
                 const std::vector<size_t>& widths) const {
-        for (size_t d = 0; d < dsts.size(); ++d) {
-            Entries m;
-            m.reserve(counts[d]);
-            for (uint32_t j = out.offsets[d]; j < out.offsets[d] + counts[d]; ++j)
-                m[*name[out.keys[j]]] = Dot{out.actors[j], out.counters[j]};
-            dsts[d]->entries = std::move(m);
-            VersionVector vv(widths[d]);
-            for (size_t r = 0; r < widths[d]; ++r) vv[r] = out.vv[d * R + r];
-            dsts[d]->versionVector = std::move(vv);
-        }
+        parallel_docs(dsts.size(), [&](size_t lo, size_t hi) {
+            for (size_t d = lo; d < hi; ++d) {
+                Entries m;
+                m.reserve(counts[d]);
+                for (uint32_t j = out.offsets[d]; j < out.offsets[d] + counts[d]; ++j)
+                    m.emplace(*names[d][out.keys[j]], Dot{out.actors[j], out.counters[j]});
+                dsts[d]->entries = std::move(m);
+                VersionVector vv(widths[d]);
+                for (size_t r = 0; r < widths[d]; ++r) vv[r] = out.vv[d * R + r];
+                dsts[d]->versionVector = std::move(vv);
+            }
+        });
     }
 };
 
@@ -265,6 +317,30 @@ inline Packed make_out(size_t n_docs, size_t R, size_t slots, std::vector<uint32
     return p;
 }
 
+// Intern a batch: doc d's states are states_of(d).
+template <typename F>
+void intern_all(Batch& b, size_t n, F&& states_of) {
+    b.names.assign(n, {});
+    parallel_docs(n, [&](size_t lo, size_t hi) {
+        for (size_t d = lo; d < hi; ++d) b.intern(d, states_of(d));
+    });
+}
+
+}  // namespace detail
+
+namespace detail {
+// Would dst.Merge(src) panic in Go at a HasDot with actor == len(vv)?  The
+// reference evaluates dstVV.HasDot(s) for every src-only key (awset.go:133)
+// and srcVV.HasDot(d) for every dst-only key (:152).  The kernels flag actor ==
+// R; this covers vectors shorter than the batch's R.
+inline bool join_panics(const AWSet& dst, const AWSet& src) {
+    const size_t ld = dst.versionVector.size(), ls = src.versionVector.size();
+    for (auto& kv : src.entries)
+        if (kv.second.actor == ld && !dst.entries.count(kv.first)) return true;
+    for (auto& kv : dst.entries)
+        if (kv.second.actor == ls && !src.entries.count(kv.first)) return true;
+    return false;
+}
 }  // namespace detail
 
 // dsts[i].Merge(*srcs[i]) for every i, as one batched GPU join.
@@ -273,9 +349,14 @@ inline void MergeBatch(const std::vector<AWSet*>& dsts, const std::vector<const 
     if (dsts.size() != srcs.size()) throw Error(CRDT_E_INVALID, "MergeBatch: length mismatch");
     if (dsts.empty()) return;
     detail::Batch b;
-    for (auto* s : dsts) b.scan(*s);
-    for (auto* s : srcs) b.scan(*s);
-    b.finish();
+    for (size_t i = 0; i < dsts.size(); ++i)
+        b.R = std::max({b.R, dsts[i]->versionVector.size(), srcs[i]->versionVector.size()});
+    if (b.R > CRDT_MAX_R) throw Error(CRDT_E_INVALID, "version vector longer than CRDT_MAX_R");
+    for (size_t i = 0; i < dsts.size(); ++i)
+        if ((dsts[i]->versionVector.size() < b.R || srcs[i]->versionVector.size() < b.R) &&
+            detail::join_panics(*dsts[i], *srcs[i]))
+            throw Error(CRDT_E_ACTOR_RANGE, "MergeBatch: HasDot at actor == len(vv)");
+    detail::intern_all(b, dsts.size(), [&](size_t d) { return std::vector<const AWSet*>{dsts[d], srcs[d]}; });
     std::vector<AWSet*> sv;
     for (auto* s : srcs) sv.push_back(const_cast<AWSet*>(s));
     detail::Packed pd = b.pack(dsts), ps = b.pack(sv);
@@ -332,21 +413,37 @@ inline void fold(int mode, const std::vector<AWSet*>& dsts, const std::vector<st
     if (dsts.size() != srcs.size()) throw Error(CRDT_E_INVALID, "fold: length mismatch");
     if (dsts.empty()) return;
     Batch b;
-    for (auto* s : dsts) b.scan(*s);
-    for (auto& l : srcs)
-        for (auto* s : l) b.scan(*s);
-    b.finish();
+    for (size_t i = 0; i < dsts.size(); ++i) {
+        b.R = std::max(b.R, dsts[i]->versionVector.size());
+        for (auto* s : srcs[i]) b.R = std::max(b.R, s->versionVector.size());
+    }
+    if (b.R > CRDT_MAX_R) throw Error(CRDT_E_INVALID, "version vector longer than CRDT_MAX_R");
+    intern_all(b, dsts.size(), [&](size_t d) {
+        std::vector<const AWSet*> v{dsts[d]};
+        v.insert(v.end(), srcs[d].begin(), srcs[d].end());
+        return v;
+    });
     Packed pd = b.pack(dsts);
     std::vector<uint32_t> doc_srcs{0}, src_actor, entry_off{0}, tomb_off{0};
     std::vector<uint64_t> vv, keys, counters, tkeys, tcounters;
     std::vector<uint32_t> actors, tactors;
-    for (auto& l : srcs) {
-        for (auto* s : l) {
+    for (size_t d = 0; d < srcs.size(); ++d) {
+        for (auto* s : srcs[d]) {
             src_actor.push_back(s->actor);
-            pack_vv(s->versionVector, b.R, vv);
-            pack_entries(s->entries, b.id, keys, actors, counters);
+            for (size_t r = 0; r < b.R; ++r) vv.push_back(r < s->versionVector.size() ? s->versionVector[r] : 0);
+            const size_t o = keys.size(), m = s->entries.size();
+            keys.resize(o + m);
+            actors.resize(o + m);
+            counters.resize(o + m);
+            b.put_entries(d, s->entries, keys.data() + o, actors.data() + o, counters.data() + o);
             entry_off.push_back((uint32_t)keys.size());
-            if (auto* del = s->deleted_map()) pack_entries(*del, b.id, tkeys, tactors, tcounters);
+            if (auto* del = s->deleted_map()) {
+                const size_t t = tkeys.size(), x = del->size();
+                tkeys.resize(t + x);
+                tactors.resize(t + x);
+                tcounters.resize(t + x);
+                b.put_entries(d, *del, tkeys.data() + t, tactors.data() + t, tcounters.data() + t);
+            }
             tomb_off.push_back((uint32_t)tkeys.size());
         }
         doc_srcs.push_back((uint32_t)src_actor.size());

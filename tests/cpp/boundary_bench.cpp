@@ -3,7 +3,8 @@
 // (map[string]Dot per replica, awset.go:55-59) pays around the kernels, phase
 // by phase, through the C++ host mirror (go-crdt-playground_amd/host/crdt.hpp,
 // the same interning and packing its MergeBatch uses):
-//   intern   string keys -> order-preserving u64 ids (one std::map per batch)
+//   intern   string keys -> order-preserving u64 ids (per document: the ranks
+//            of the document's keys; documents spread over host threads)
 //   pack     maps -> sorted SoA arrays (keys, actors, counters, offsets, vv)
 //   h2d      pageable host -> HBM copies of both states
 //   kernel   the exchange (A<-B and B<-A from one read), device time
@@ -56,6 +57,12 @@ static T* dev_alloc(size_t n) {
     return hipMalloc(&p, std::max<size_t>(n, 1) * sizeof(T)) == hipSuccess ? p : nullptr;
 }
 
+static size_t keys_interned(const detail::Batch& b) {
+    size_t k = 0;
+    for (auto& v : b.names) k += v.size();
+    return k;
+}
+
 int main(int argc, char** argv) {
     const size_t n = argc > 1 ? strtoull(argv[1], nullptr, 10) : 65536;
     const int E = 64;
@@ -83,9 +90,8 @@ int main(int argc, char** argv) {
 
     auto t0 = clk::now();
     detail::Batch b;
-    for (auto* s : pa) b.scan(*s);
-    for (auto* s : pb) b.scan(*s);
-    b.finish();
+    b.R = 2;
+    detail::intern_all(b, n, [&](size_t d) { return std::vector<const AWSet*>{pa[d], pb[d]}; });
     auto t1 = clk::now();
     detail::Packed xa = b.pack(pa), xb = b.pack(pb);
     auto t2 = clk::now();
@@ -153,9 +159,9 @@ int main(int argc, char** argv) {
     const double total = intern + pack + h2d + kernel + d2h + unpack;
     printf("{\"docs\": %zu, \"entries_per_replica\": %d, \"keys_interned\": %zu, \"out_entries_per_doc\": %.2f, "
            "\"intern_s\": %.6f, \"pack_s\": %.6f, \"h2d_s\": %.6f, \"kernel_s\": %.6f, \"d2h_s\": %.6f, "
-           "\"unpack_s\": %.6f, \"end_to_end_merges_per_s\": %.1f, \"kernel_only_merges_per_s\": %.1f, "
+           "\"unpack_s\": %.6f, \"host_threads\": %u, \"end_to_end_merges_per_s\": %.1f, \"kernel_only_merges_per_s\": %.1f, "
            "\"pcie_inclusive_merges_per_s\": %.1f}\n",
-           n, E, b.name.size(), (double)live / n, intern, pack, h2d, kernel, d2h, unpack, merges / total,
+           n, E, keys_interned(b), (double)live / n, intern, pack, h2d, kernel, d2h, unpack, detail::host_threads(), merges / total,
            merges / kernel, merges / (h2d + kernel + d2h));
     crdt_ctx_destroy(ctx);
     return 0;

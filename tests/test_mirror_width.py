@@ -48,3 +48,31 @@ def test_delta_fold_width_matches_reference():
         checked += 1
         shorter += want < max([len(vv)] + [len(c[2]) for c in chain])
     assert checked > 1000 and shorter > 5  # the no-op rule really kept some VVs short
+
+
+def test_join_panic_check_matches_reference_for_unequal_lengths():
+    """Zero-padded VVs hide Go's panic at HasDot(actor == len(vv)) of the shorter
+    vector from the kernels (they flag actor == R); the mirrors find it on the
+    host (awset.py _join_panics, crdt.hpp detail::join_panics).  Exactly where
+    the map-based restatement raises GoPanic."""
+    from crdtgpu.awset import AWSet, _join_panics
+
+    rng = random.Random(72)
+    panics = 0
+    for _ in range(4000):
+        ea, va, _ = _rand(rng, rng.randint(1, 4), 8, False)
+        eb, vb, _ = _rand(rng, rng.randint(1, 4), 8, False)
+        # actors up to 4 so that actor == len(shorter vv) happens often
+        ea = [(k, rng.randrange(5), c) for k, _, c in ea]
+        eb = [(k, rng.randrange(5), c) for k, _, c in eb]
+        x, y = ref_state(ea, va), ref_state(eb, vb)
+        try:
+            x.Merge(y)
+            want = False
+        except ref.GoPanic:
+            want = True
+        a = AWSet(0, va, {"%012d" % k: Dot(p, c) for k, p, c in ea})
+        b = AWSet(1, vb, {"%012d" % k: Dot(p, c) for k, p, c in eb})
+        assert _join_panics(a, b) == want
+        panics += want
+    assert panics > 200

@@ -30,8 +30,9 @@ def main():
     o1, o2 = OutBuffers(n, 2, 2 * total, device=dev), OutBuffers(n, 2, 2 * total, device=dev)
     a, b = A.as_batch(), B.as_batch()
     ref = None
-    for shape in (0, 1, 2, 3, 0):
+    for shape, nts in ((2, 0), (2, 1), (0, 0), (0, 1), (1, 0), (3, 0), (2, 0)):
         eng.set_option("join_tile_shape", shape)
+        eng.set_option("join_tile_nt_stores", nts)
         eng.exchange_async(a, b, o1, o2)
         eng.sync()
         got = (o1.counts.clone(), o1.keys[:: 9973].clone(), o2.counters[:: 9973].clone())
@@ -44,7 +45,8 @@ def main():
             eng.exchange_async(a, b, o1, o2)
         ev[1].record()
         eng.sync()
-        print("shape %d: %.3f ms per exchange call (same output: %s)" % (shape, ev[0].elapsed_time(ev[1]) / 5, same),
+        print("shape %d nt %d: %.3f ms per exchange call (same output: %s)" % (shape, nts, ev[0].elapsed_time(ev[1]) / 5,
+                                                                          same),
               flush=True)
     eng.close()
 
