@@ -447,7 +447,7 @@ def run_config(config, n, args, ctx, steps, warmup, repeats, cpu):
     # The dominant launch is captured once into a HIP graph and replayed each
     # step: one host call per step instead of the ABI calls of every kernel.
     # Before timing, the replayed output is compared bitwise with an eager launch.
-    graph, replay_check, graph_error = None, None, None
+    graph, post_graph, replay_check, graph_error, graph_ctx = None, None, None, None, None
     if not args.no_graph:
         try:
             for t in W.outputs():  # poison, so a replay that writes nothing cannot pass
@@ -458,6 +458,9 @@ def run_config(config, n, args, ctx, steps, warmup, repeats, cpu):
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
                 W.hot(torch.cuda.current_stream())
+            gp = torch.cuda.CUDAGraph()  # the per-GPU causal-context summary, its own graph
+            with torch.cuda.graph(gp):
+                graph_ctx = W.post(torch.cuda.current_stream())
             torch.cuda.synchronize()
             for t in W.outputs():
                 t.fill_(-1)
@@ -465,7 +468,7 @@ def run_config(config, n, args, ctx, steps, warmup, repeats, cpu):
             torch.cuda.synchronize()
             replay_check = all(bool(torch.equal(a, b)) for a, b in zip(eager, W.outputs()))
             del eager
-            graph = g
+            graph, post_graph = g, gp
         except Exception as e:  # capture refused: report it and launch eagerly
             graph_error = "%s: %s" % (type(e).__name__, e)
             torch.cuda.synchronize()
@@ -479,15 +482,22 @@ def run_config(config, n, args, ctx, steps, warmup, repeats, cpu):
             W.hot(stream)
         if ev is not None:
             ev[1].record(stream)
-        local_ctx = W.post(stream)
+        if graph is not None:
+            post_graph.replay()
+            local_ctx = graph_ctx
+        else:
+            local_ctx = W.post(stream)
         if dist is not None:
             return u64_max_allreduce(dist, local_ctx)
         return local_ctx
 
-    for _ in range(warmup):
-        step()
+    if graph is None:
+        W.hot(stream)
     eng.sync(stream)
     bytes_launch, per_merge_bytes = W.bytes_per_launch()  # from the actual output sizes
+    for _ in range(warmup):  # right before the timed steps, no host pause in between
+        step()
+    eng.sync(stream)
 
     def timed():
         events = [[torch.cuda.Event(enable_timing=True) for _ in range(2)] for _ in range(steps)]
@@ -544,7 +554,7 @@ def run_config(config, n, args, ctx, steps, warmup, repeats, cpu):
         res["roofline"]["traffic_frac"] = traffic / t_launch / 1e9 / HBM_PEAK_GBS
     if cpu and rank == 0 and world == 1:
         res["cpu_baseline"] = W.cpu_baseline(args.cpu_budget)
-    del graph, W
+    del graph, post_graph, W
     torch.cuda.synchronize()
     torch.cuda.empty_cache()
     return res
@@ -576,14 +586,14 @@ def boundary_cost(n_docs):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=100)
-    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--steps", type=int, default=400)
+    ap.add_argument("--warmup", type=int, default=100)
     ap.add_argument("--config", type=int, default=2, choices=[2, 3, 4, 5], help="the headline workload")
     ap.add_argument("--legs", default=None,
                     help="comma-separated configs timed after the headline (default with --config 2: 3,4,5; "
                          "otherwise none); 'none' for the headline only")
     ap.add_argument("--leg-steps", type=int, default=20)
-    ap.add_argument("--leg-warmup", type=int, default=3)
+    ap.add_argument("--leg-warmup", type=int, default=5)
     ap.add_argument("--repeats", type=int, default=3, help="timed runs of the headline (the first is the value)")
     ap.add_argument("--docs", type=int, default=None, help="documents per GPU for the headline")
     ap.add_argument("--seed", type=int, default=0x5EED)

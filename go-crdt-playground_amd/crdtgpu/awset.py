@@ -286,3 +286,62 @@ def DeltaMergeBatch(dsts: Sequence[AWSetDelta], srcs_per_dst: Sequence[Sequence[
                     engine: Optional[Engine] = None):
     """for each i, for src in srcs_per_dst[i] in order: dsts[i].Merge(src) (AWSetDelta semantics)."""
     _fold(abi.CRDT_FOLD_DELTA, dsts, srcs_per_dst, engine)
+
+
+def ApplyBatch(states: Sequence[AWSet], calls_per_state: Sequence[Sequence[tuple]],
+               engine: Optional[Engine] = None) -> None:
+    """Local ops on many replicas in one GPU call (crdt_awset_apply_batch).
+
+    calls_per_state[i] is state i's call script, applied in order:
+      ("Add", k1, k2, ...)        (*AWSet).Add          awset.go:89-94
+      ("Del", k1, ...)            Del of the state's own type: (*AWSetDelta).Del
+                                  (awset-delta_test.go:14-33) for an AWSetDelta,
+                                  (*AWSet).Del (awset.go:96-101) otherwise
+      ("AWSet.Del", k1, ...)      the embedded (*AWSet).Del of an AWSetDelta
+    A call that bumps the clock with Actor >= len(VersionVector) is Go's index
+    panic: CrdtError(CRDT_E_ACTOR_RANGE), nothing applied.  Each state's script
+    holds at most CRDT_MAX_OPS_PER_DOC ops (one per key, plus one per delta Del)."""
+    from .batch import OpBatch, TombBatch
+
+    if len(states) != len(calls_per_state):
+        raise ValueError("ApplyBatch: length mismatch")
+    if not states:
+        return
+    R = _width(states)
+    per_ops, tombs = [], []
+    for s, calls in zip(states, calls_per_state):
+        ops = []
+        for call in calls:
+            name, keys = call[0], call[1:]
+            delta_del = name == "Del" and isinstance(s, AWSetDelta)
+            if (name == "Add" and keys) or delta_del:  # clock bump: vv[actor]++ panics past the end
+                if s.Actor >= len(s.VersionVector):
+                    raise abi.CrdtError(abi.CRDT_E_ACTOR_RANGE, "ApplyBatch: %s with actor %d" % (name, s.Actor))
+            if name == "Add":
+                ops += [(abi.CRDT_OP_ADD, k) for k in keys]
+            elif delta_del:
+                ops.append((abi.CRDT_OP_DELTA_DEL, None))
+                ops += [(abi.CRDT_OP_DELTA_DEL_KEY, k) for k in keys]
+            elif name in ("Del", "AWSet.Del"):
+                ops += [(abi.CRDT_OP_DEL, k) for k in keys]
+            else:
+                raise ValueError("ApplyBatch: unknown call %r" % (name,))
+        per_ops.append(ops)
+    # keys interned per batch (order-preserving over states, tombstones and op keys)
+    names_all = set()
+    for s, ops in zip(states, per_ops):
+        names_all.update(s.Entries)
+        names_all.update(getattr(s, "Deleted", None) or {})
+        names_all.update(k for _, k in ops if k is not None)
+    ids = {k: i for i, k in enumerate(sorted(names_all))}
+    names = {i: k for k, i in ids.items()}
+    st = AWSetBatch.from_docs(R, [(_entries(s.Entries, ids), _pad(s.VersionVector, R)) for s in states])
+    tb = TombBatch.from_lists([_entries(getattr(s, "Deleted", None), ids) for s in states])
+    ob = OpBatch.from_lists([[(k, ids[key] if key is not None else 0) for k, key in ops] for ops in per_ops],
+                            [s.Actor for s in states])
+    out, tout = (engine or default_engine()).apply(st, ob, tb)
+    _unpack(states, out, names, R, [len(s.VersionVector) for s in states])
+    for d, s in enumerate(states):
+        if isinstance(s, AWSetDelta):
+            dele = {names[k]: Dot(a, c) for k, a, c in tout.doc(d)}
+            s.Deleted = dele if (dele or s.Deleted is not None) else None  # nil until the first record

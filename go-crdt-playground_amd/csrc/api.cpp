@@ -101,7 +101,7 @@ struct crdt_ctx {
     DevBuf scratch;  // fold block path ping-pong: keys | actors | counters
     // large-document join tiles (tile.hip): descriptors + look-back words for
     // tile_cap tiles, per-slot and per-run tile counts for the worklist
-    DevBuf tile_desc, tile_flags, tile_slot, tile_run;
+    DevBuf tile_desc, tile_geo, tile_flags, tile_slot, tile_run;
     uint32_t tile_cap = 1u << 20;             // crdt_ctx_set_option("join_tile_capacity")
     bool join_tiles = true;                   // crdt_ctx_set_option("join_tiles")
     uint32_t tile_shape = 2;                  // crdt_ctx_set_option("join_tile_shape")
@@ -250,7 +250,7 @@ int crdt_ctx_create(int device, crdt_ctx** out) {
     crdt_ctx* ctx = new (std::nothrow) crdt_ctx();
     if (!ctx) return CRDT_E_NOMEM;
     ctx->device = device;
-    for (DevBuf* b : {&ctx->ws, &ctx->worklist, &ctx->parts, &ctx->scratch, &ctx->tile_desc, &ctx->tile_flags,
+    for (DevBuf* b : {&ctx->ws, &ctx->worklist, &ctx->parts, &ctx->scratch, &ctx->tile_desc, &ctx->tile_geo, &ctx->tile_flags,
                       &ctx->tile_slot, &ctx->tile_run})
         b->retired = &ctx->retired;
     for (auto& b : ctx->stage) b.retired = &ctx->retired;
@@ -285,7 +285,7 @@ void crdt_ctx_destroy(crdt_ctx* ctx) {
     ctx->worklist.release();
     ctx->parts.release();
     ctx->scratch.release();
-    for (DevBuf* b : {&ctx->tile_desc, &ctx->tile_flags, &ctx->tile_slot, &ctx->tile_run}) b->release();
+    for (DevBuf* b : {&ctx->tile_desc, &ctx->tile_geo, &ctx->tile_flags, &ctx->tile_slot, &ctx->tile_run}) b->release();
     for (auto& b : ctx->stage) b.release();
     delete ctx;
 }
@@ -375,12 +375,13 @@ static int join_common(crdt_ctx* ctx, const crdt_awset_batch* dst, const crdt_aw
     if (tiles) {
         const size_t n = std::max<size_t>(dst->n_docs, 1);
         rc = grow(ctx->tile_desc, (size_t)ctx->tile_cap * 16, cap);
+        if (rc == CRDT_OK) rc = grow(ctx->tile_geo, (size_t)ctx->tile_cap * 32, cap);
         if (rc == CRDT_OK) rc = grow(ctx->tile_flags, (size_t)ctx->tile_cap * 8, cap);
         if (rc == CRDT_OK) rc = grow(ctx->tile_slot, n * 4, cap);
         if (rc == CRDT_OK) rc = grow(ctx->tile_run, ((n + 1023) / 1024) * 4, cap);
         if (rc != CRDT_OK) return rc;
         uint32_t* w = ctx->ws.as<uint32_t>(0);
-        tw = TileWork{ctx->tile_desc.as<uint4>(), ctx->tile_flags.as<uint64_t>(), ctx->tile_slot.as<uint32_t>(),
+        tw = TileWork{ctx->tile_desc.as<uint4>(), ctx->tile_geo.as<uint4>(), ctx->tile_flags.as<uint64_t>(), ctx->tile_slot.as<uint32_t>(),
                       ctx->tile_run.as<uint32_t>(), w + 3, w + 4, w + 5, ctx->tile_cap,
                       tile_positions(ctx->tile_shape), ctx->tile_shape, ctx->tile_nt_stores ? 1u : 0u};
     }

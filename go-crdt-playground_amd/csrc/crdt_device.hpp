@@ -100,6 +100,7 @@ struct TombOut {
 // Workspace of the large-document tile path (tile.hip).
 struct TileWork {
     uint4* desc;          // [cap] {doc, tile index in doc, i0, j0}
+    uint4* geo;           // [2*cap] per-tile geometry (tile.hip, tile_geo_kernel)
     uint64_t* flags;      // [cap] look-back words
     uint32_t* slot_incl;  // [n_docs] inclusive tile count within the slot's run
     uint32_t* run;        // [ceil(n_docs/kRun)] run sums -> exclusive prefixes

@@ -186,36 +186,58 @@ __device__ __forceinline__ uint32_t look_back(uint64_t* flags, uint32_t g, uint3
 
 // A tile's coordinates, from its descriptor and its successor's (uniform loads).
 struct TileGeo {
-    uint32_t d, t, i0, j0, nA, nB, ns, aoff, boff;
-    bool last, bad;
+    uint32_t d, t, ga, gb, nA, nB, obase;  // ga/gb: absolute slot of the tile's first dst/src element
+    bool last, has_next, has_prev, bad;
 };
 
-__device__ __forceinline__ TileGeo tile_geo(const BatchView& A, const BatchView& B, const TileWork& tw, uint32_t g,
-                                            uint32_t total) {
-    TileGeo x{};
-    const uint4 ds = tw.desc[g];
-    x.d = ds.x;
-    x.t = ds.y;
-    x.i0 = ds.z;
-    x.j0 = ds.w;
-    x.last = true;
-    x.bad = x.d >= A.n_docs;  // not a document of this call: never dereferenced
-    if (x.bad) return x;
-    const uint32_t nd = live_count(A.offsets, A.counts, x.d);
-    x.ns = live_count(B.offsets, B.counts, x.d);
-    x.aoff = A.offsets[x.d];
-    x.boff = B.offsets[x.d];
-    uint32_t i1 = nd, j1 = x.ns;
-    if (g + 1 < total) {
-        const uint4 nx = tw.desc[g + 1];
-        if (nx.x == x.d && nx.y == x.t + 1) {
-            i1 = nx.z;
-            j1 = nx.w;
-            x.last = false;
+// Per-tile geometry, precomputed once per call (tile_geo_kernel) so that a
+// workgroup's dependent chain per tile is dispense -> one 32-byte record ->
+// data loads.
+__global__ __launch_bounds__(256) void tile_geo_kernel(BatchView A, BatchView B, TileWork tw) {
+    const uint32_t total = *tw.total;
+    for (uint32_t g = blockIdx.x * 256 + threadIdx.x; g < total; g += gridDim.x * 256) {
+        const uint4 ds = tw.desc[g];
+        const uint32_t d = ds.x, t = ds.y, i0 = ds.z, j0 = ds.w;
+        uint4 r0 = make_uint4(d, t, 0u, 0u), r1 = make_uint4(0u, 0u, 1u, 0u);
+        if (d < A.n_docs) {
+            const uint32_t nd = live_count(A.offsets, A.counts, d), ns = live_count(B.offsets, B.counts, d);
+            const uint32_t aoff = A.offsets[d], boff = B.offsets[d];
+            uint32_t i1 = nd, j1 = ns, last = 1u;
+            if (g + 1 < total) {
+                const uint4 nx = tw.desc[g + 1];
+                if (nx.x == d && nx.y == t + 1) {
+                    i1 = nx.z;
+                    j1 = nx.w;
+                    last = 0u;
+                }
+            }
+            r0.z = aoff + i0;
+            r0.w = boff + j0;
+            r1.x = i1 - i0;
+            r1.y = j1 - j0;
+            r1.z = last | (j1 < ns ? 2u : 0u) | (i0 > 0 ? 4u : 0u);
+            r1.w = aoff + boff;
         }
+        tw.geo[2 * (size_t)g] = r0;
+        tw.geo[2 * (size_t)g + 1] = r1;
     }
-    x.nA = i1 - x.i0;
-    x.nB = j1 - x.j0;
+}
+
+__device__ __forceinline__ TileGeo tile_geo(const BatchView& A, const TileWork& tw, uint32_t g) {
+    TileGeo x{};
+    const uint4 r0 = tw.geo[2 * (size_t)g], r1 = tw.geo[2 * (size_t)g + 1];
+    x.d = r0.x;
+    x.t = r0.y;
+    x.ga = r0.z;
+    x.gb = r0.w;
+    x.nA = r1.x;
+    x.nB = r1.y;
+    x.last = (r1.z & 1u) != 0;
+    x.has_next = (r1.z & 2u) != 0;
+    x.has_prev = (r1.z & 4u) != 0;
+    x.obase = r1.w;
+    x.bad = x.d >= A.n_docs;  // not a document of this call: never dereferenced
+    if (x.bad) x.nA = x.nB = 0, x.has_next = x.has_prev = false;
     return x;
 }
 
@@ -230,13 +252,13 @@ __device__ __forceinline__ void tile_issue(const BatchView& A, const BatchView& 
                                            uint64_t& xk, uint32_t& xa, uint64_t& xc, uint64_t& pk) {
     constexpr uint32_t T = NT * IPT;
     const uint32_t n = x.nA + x.nB;
-    const bool peek = !x.bad && x.j0 + x.nB < x.ns;
-    const uint64_t* ak = A.keys + x.aoff + x.i0;
-    const uint32_t* aa = A.actors + x.aoff + x.i0;
-    const uint64_t* ac = A.counters + x.aoff + x.i0;
-    const uint64_t* bk = B.keys + x.boff + x.j0;
-    const uint32_t* ba = B.actors + x.boff + x.j0;
-    const uint64_t* bc = B.counters + x.boff + x.j0;
+    const bool peek = x.has_next;
+    const uint64_t* ak = A.keys + x.ga;
+    const uint32_t* aa = A.actors + x.ga;
+    const uint64_t* ac = A.counters + x.ga;
+    const uint64_t* bk = B.keys + x.gb;
+    const uint32_t* ba = B.actors + x.gb;
+    const uint64_t* bc = B.counters + x.gb;
 #pragma unroll
     for (int q = 0; q < IPT; ++q) {
         const uint32_t p = tid + q * NT;
@@ -257,7 +279,7 @@ __device__ __forceinline__ void tile_issue(const BatchView& A, const BatchView& 
             xa = ba[x.nB];
             xc = bc[x.nB];
         }
-        if (!x.bad && x.i0 > 0) pk = ak[-1];
+        if (x.has_prev) pk = ak[-1];
     }
 }
 
@@ -291,7 +313,7 @@ __global__ __launch_bounds__(NT) void join_tile_kernel(BatchView A, BatchView B,
     uint32_t g = sm.word[0];
     TileGeo x{};
     if (g < total) {
-        x = tile_geo(A, B, tw, g, total);
+        x = tile_geo(A, tw, g);
         tile_issue<NT, IPT>(A, B, x, tid, rk, ra, rc, xk, xa, xc, pk);
     }
     while (g < total) {
@@ -321,7 +343,7 @@ __global__ __launch_bounds__(NT) void join_tile_kernel(BatchView A, BatchView B,
             sm.vb[tid] = B.vv[(size_t)d * R + tid];
         }
         __syncthreads();
-        const bool has_next = !cur.bad && cur.j0 + nB < cur.ns, has_prev = !cur.bad && cur.i0 > 0;
+        const bool has_next = cur.has_next, has_prev = cur.has_prev;
         const uint64_t prev_key = sm.prev_key;
 
         // merge IPT positions from this thread's diagonal split
@@ -398,11 +420,11 @@ __global__ __launch_bounds__(NT) void join_tile_kernel(BatchView A, BatchView B,
         const uint32_t prefix = sm.word[1];
         const uint32_t gn = sm.word[0];
         if (gn < total) {  // the next tile's loads overlap this tile's stores
-            x = tile_geo(A, B, tw, gn, total);
+            x = tile_geo(A, tw, gn);
             tile_issue<NT, IPT>(A, B, x, tid, rk, ra, rc, xk, xa, xc, pk);
         }
         if (!cur.bad) {
-            const size_t obase = (size_t)cur.aoff + cur.boff + prefix;
+            const size_t obase = (size_t)cur.obase + prefix;
 #pragma unroll
             for (int q = 0; q < IPT; ++q) {
                 const uint32_t p = tid + q * NT;
@@ -485,6 +507,9 @@ hipError_t launch_join_tiles(const BatchView& A, const BatchView& B, const OutVi
     e = hipGetLastError();
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL((tile_split_kernel<256>), dim3(n_cu * 4), dim3(256), 0, stream, A, B, wk, tw);
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(tile_geo_kernel, dim3(n_cu * 4), dim3(256), 0, stream, A, B, tw);
     e = hipGetLastError();
     if (e != hipSuccess) return e;
     switch (tw.shape) {

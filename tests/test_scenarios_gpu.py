@@ -177,3 +177,55 @@ def test_batch_entry_points():
     y.Add("k")
     DeltaMergeBatch([x], [[y]])
     assert x.Entries == {"k": Dot(1, 1)} and list(x.VersionVector) == [0, 1]
+
+
+def test_apply_batch_matches_reference_calls():
+    """ApplyBatch (batched Add / Del / AWSetDelta.Del on the GPU) leaves every
+    replica exactly as the same calls on the map-based restatement
+    (oracle/awset_ref.py) do: entries, Deleted, clocks; panics raise and leave
+    the replica untouched."""
+    import random
+
+    from crdtgpu import CrdtError
+    from crdtgpu.awset import ApplyBatch
+    from oracle import awset_ref as ref
+
+    rng = random.Random(9)
+    keys = ["k%02d" % i for i in range(30)]
+    mirrors, refs, scripts = [], [], []
+    for i in range(300):
+        R = rng.randint(1, 4)
+        actor = rng.randrange(R)
+        delta = i % 2 == 0
+        m = (AWSetDelta if delta else AWSet)(actor, [rng.randint(0, 5) for _ in range(R)])
+        r = (ref.AWSetDelta if delta else ref.AWSet)(actor, ref.VersionVector(list(m.VersionVector)))
+        for k in rng.sample(keys, rng.randint(0, 10)):  # a starting state, same on both
+            m.Add(k)
+            r.Add(k)
+        calls = []
+        for _ in range(rng.randint(0, 12)):
+            name = rng.choice(["Add", "Del", "AWSet.Del"] if delta else ["Add", "Del"])
+            calls.append((name,) + tuple(rng.sample(keys, rng.randint(0, 3))))
+        for c in calls:
+            if c[0] == "Add":
+                r.Add(*c[1:])
+            elif c[0] == "AWSet.Del":
+                ref.AWSet.Del(r, *c[1:])
+            else:
+                r.Del(*c[1:])
+        mirrors.append(m)
+        refs.append(r)
+        scripts.append(calls)
+    ApplyBatch(mirrors, scripts)
+    for m, r in zip(mirrors, refs):
+        assert {k: (d.Actor, d.Counter) for k, d in m.Entries.items()} == \
+            {k: (d.actor, d.counter) for k, d in r.Entries.items()}
+        assert list(m.VersionVector) == list(r.VersionVector)
+        if isinstance(m, AWSetDelta):
+            assert {k: (d.Actor, d.Counter) for k, d in (m.Deleted or {}).items()} == \
+                {k: (d.actor, d.counter) for k, d in (r.Deleted or {}).items()}
+    # panic: Add with the actor outside a shorter vector (the batch pads to R = 3)
+    a, b = AWSet(2, [0, 0]), AWSet(0, [0, 0, 0])
+    with pytest.raises(CrdtError):
+        ApplyBatch([a, b], [[("Add", "x")], [("Add", "y")]])
+    assert a.Entries == {} and list(a.VersionVector) == [0, 0]
