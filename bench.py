@@ -437,6 +437,7 @@ def run_config(config, n, args, ctx, steps, warmup, repeats, cpu):
     from crdtgpu.dist import u64_max_allreduce
 
     eng, dev, stream, dist, world, rank = ctx
+    backend_is_host = dist is not None and dist.get_backend() != "nccl"
     seed = args.seed + (rank << 40)  # each rank owns its own documents (weak scaling)
     cls = CONFIGS[config]
     if args.separate and config in (2, 4):
@@ -488,6 +489,8 @@ def run_config(config, n, args, ctx, steps, warmup, repeats, cpu):
         else:
             local_ctx = W.post(stream)
         if dist is not None:
+            if backend_is_host:
+                return u64_max_allreduce(dist, local_ctx.cpu()).to(dev)
             return u64_max_allreduce(dist, local_ctx)
         return local_ctx
 
@@ -513,7 +516,7 @@ def run_config(config, n, args, ctx, steps, warmup, repeats, cpu):
             dist.barrier()
         el = time.perf_counter() - t0
         if dist is not None:
-            t = torch.tensor([el], dtype=torch.float64, device=dev)
+            t = torch.tensor([el], dtype=torch.float64, device="cpu" if backend_is_host else dev)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             el = float(t.item())
         # mean duration of one launch of the dominant kernel, HIP events on its stream
@@ -614,15 +617,23 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    # CRDT_BENCH_DIST_BACKEND=gloo: a rehearsal of the multi-rank path on a box
+    # with fewer GPUs than ranks (ranks share GPUs; collectives on host copies).
+    # The driver's runs use nccl (RCCL), one GPU per rank.
+    backend = os.environ.get("CRDT_BENCH_DIST_BACKEND", "nccl")
+    gpu = local if backend == "nccl" else local % max(1, torch.cuda.device_count())
     if world > 1:
         import torch.distributed as dist
 
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
+        torch.cuda.set_device(gpu)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
+        else:
+            dist.init_process_group(backend)
+    dev = torch.device("cuda", gpu)
     torch.cuda.set_device(dev)
     stream = torch.cuda.current_stream()
-    eng = crdtgpu.Engine(local)
+    eng = crdtgpu.Engine(gpu)
     ctx = (eng, dev, stream, dist, world, rank)
 
     if args.legs is None:

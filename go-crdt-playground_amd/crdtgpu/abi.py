@@ -24,6 +24,7 @@ CRDT_E_HIP = -5
 CRDT_E_NOMEM = -6
 CRDT_E_WORKSPACE = -7
 CRDT_E_RCCL = -8
+CRDT_E_DUP_KEY = -9
 CRDT_COMM_ID_BYTES = 128
 CRDT_MAX_R = 64
 CRDT_FOLD_AWSET = 0
@@ -145,6 +146,8 @@ def _load():
                                                   P(CTombOut), _vp]),
         "crdt_awset_apply_batch": (ctypes.c_int, [_vp, P(CAWSetBatch), P(CTombBatch), P(COpBatch), P(CAWSetOut),
                                                   P(CTombOut)]),
+        "crdt_awset_sort_async": (ctypes.c_int, [_vp, P(CAWSetBatch), _u32, P(CAWSetOut), _vp]),
+        "crdt_awset_sort_batch": (ctypes.c_int, [_vp, P(CAWSetBatch), P(CAWSetOut)]),
         "crdt_tombstone_gc_async": (ctypes.c_int, [_vp, P(CTombBatch), _u32, _u32, _vp, P(CTombOut), _vp]),
         "crdt_vv_min_async": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_size_t, _vp]),
         "crdt_awset_format": (ctypes.c_int, [P(CAWSetBatch), _u32, _vp, _vp, ctypes.c_size_t,

@@ -96,6 +96,20 @@ class Engine:
                                                ctypes.byref(cto) if cto else None, _stream(stream)),
               "crdt_awset_apply_async")
 
+    def sort_async(self, batch: AWSetBatch, n_slots: int, out: OutBuffers, stream=None):
+        """Ingest sort: each doc's live entries ordered by key (crdt_awset_sort_async)."""
+        cb, co = _c(batch), _c(out)
+        check(self._lib.crdt_awset_sort_async(self._ctx, ctypes.byref(cb), int(n_slots), ctypes.byref(co),
+                                              _stream(stream)), "crdt_awset_sort_async")
+
+    def sort(self, batch: AWSetBatch) -> OutBuffers:
+        """Host buffers: the batch with each doc's live entries sorted by key."""
+        b = batch.numpy()
+        out = OutBuffers(b.n_docs, b.R, int(b.offsets[-1]))
+        cb, co = b.c(), out.c()
+        check(self._lib.crdt_awset_sort_batch(self._ctx, ctypes.byref(cb), ctypes.byref(co)), "crdt_awset_sort_batch")
+        return out
+
     def tombstone_gc_async(self, tombs: TombBatch, R: int, stable_vv, out: TombBuffers, stream=None):
         """Opt-in GC: drop each doc's tombstones its stable clock covers (crdt_tombstone_gc_async)."""
         ct, co = _c(tombs), out.c_out()

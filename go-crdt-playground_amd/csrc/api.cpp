@@ -18,6 +18,9 @@ hipError_t launch_join(const BatchView& dst, const BatchView& src, const OutView
 hipError_t launch_fold(int mode, const BatchView& dst, const SrcView& sb, const OutView& out, const Scratch& scr,
                        const Work& wk, uint32_t block_grid, hipStream_t stream);
 uint32_t tile_positions(uint32_t shape);
+hipError_t sort_storage(uint32_t n_docs, uint32_t n_slots, size_t* bytes);
+hipError_t launch_sort(const BatchView& in, uint32_t n_slots, const OutView& out, void* temp, size_t temp_bytes,
+                       uint32_t* ends, uint32_t* idx, uint32_t* status, uint32_t n_cu, hipStream_t stream);
 hipError_t launch_apply(const BatchView& st, const TombView& tb, const ApplyOps& ops, const OutView& out,
                         const TombOut& tout, bool has_tout, const Work& wk, uint32_t n_cu, hipStream_t stream);
 hipError_t launch_vv_max(uint64_t* dst, const uint64_t* src, size_t n, hipStream_t stream);
@@ -102,6 +105,7 @@ struct crdt_ctx {
     // large-document join tiles (tile.hip): descriptors + look-back words for
     // tile_cap tiles, per-slot and per-run tile counts for the worklist
     DevBuf tile_desc, tile_geo, tile_flags, tile_slot, tile_run;
+    DevBuf sort_tmp, sort_idx, sort_ends;  // ingest sort (sort.hip)
     uint32_t tile_cap = 1u << 20;             // crdt_ctx_set_option("join_tile_capacity")
     bool join_tiles = true;                   // crdt_ctx_set_option("join_tiles")
     uint32_t tile_shape = 2;                  // crdt_ctx_set_option("join_tile_shape")
@@ -240,6 +244,7 @@ const char* crdt_strerror(int code) {
         case CRDT_E_NOMEM: return "device allocation failed";
         case CRDT_E_WORKSPACE: return "fold scratch too small: call crdt_ctx_reserve with the output slot count";
         case CRDT_E_RCCL: return "RCCL unavailable or a collective failed";
+        case CRDT_E_DUP_KEY: return "a key appears twice in one document";
         default: return "unknown error";
     }
 }
@@ -251,7 +256,7 @@ int crdt_ctx_create(int device, crdt_ctx** out) {
     if (!ctx) return CRDT_E_NOMEM;
     ctx->device = device;
     for (DevBuf* b : {&ctx->ws, &ctx->worklist, &ctx->parts, &ctx->scratch, &ctx->tile_desc, &ctx->tile_geo, &ctx->tile_flags,
-                      &ctx->tile_slot, &ctx->tile_run})
+                      &ctx->tile_slot, &ctx->tile_run, &ctx->sort_tmp, &ctx->sort_idx, &ctx->sort_ends})
         b->retired = &ctx->retired;
     for (auto& b : ctx->stage) b.retired = &ctx->retired;
     int rc = set_device(ctx);
@@ -353,6 +358,7 @@ int crdt_ctx_sync(crdt_ctx* ctx, void* stream) {
         if (status & kErrWorkspace) return CRDT_E_WORKSPACE;
         if (status & kErrHint) return CRDT_E_INVALID;
         if (status & kErrCapacity) return CRDT_E_CAPACITY;
+        if (status & kErrDupKey) return CRDT_E_DUP_KEY;
     }
     return CRDT_OK;
 }
@@ -453,6 +459,28 @@ int crdt_awset_apply_async(crdt_ctx* ctx, const crdt_awset_batch* state, const c
     const ApplyOps av{ops->n_docs, ops->op_off, ops->kind, ops->keys, ops->doc_actor};
     rc = hip_err(launch_apply(view(state), tv, av, view(out), to, tomb_out != nullptr, make_work(ctx),
                               (uint32_t)ctx->n_cu, s));
+    return leave(ctx, s, cap, rc);
+}
+
+int crdt_awset_sort_async(crdt_ctx* ctx, const crdt_awset_batch* in, uint32_t n_slots, const crdt_awset_out* out,
+                          void* stream) {
+    if (!ctx || !batch_ptrs_ok(in) || !out_ptrs_ok(out) || out->keys == in->keys) return CRDT_E_INVALID;
+    if (n_slots && (!in->keys || !in->actors || !in->counters)) return CRDT_E_INVALID;
+    int rc = set_device(ctx);
+    if (rc != CRDT_OK) return rc;
+    hipStream_t s = (hipStream_t)stream;
+    bool cap = false;
+    rc = enter(ctx, s, cap);
+    if (rc != CRDT_OK) return rc;
+    size_t tb = 0;
+    if (sort_storage(in->n_docs, n_slots, &tb) != hipSuccess) return CRDT_E_HIP;
+    rc = grow(ctx->sort_tmp, std::max<size_t>(tb, 16), cap);
+    if (rc == CRDT_OK) rc = grow(ctx->sort_idx, std::max<size_t>(n_slots, 1) * 4, cap);
+    if (rc == CRDT_OK) rc = grow(ctx->sort_ends, std::max<size_t>(in->n_docs, 1) * 4, cap);
+    if (rc != CRDT_OK) return rc;
+    rc = hip_err(launch_sort(view(in), n_slots, view(out), ctx->sort_tmp.p, ctx->sort_tmp.bytes,
+                             ctx->sort_ends.as<uint32_t>(), ctx->sort_idx.as<uint32_t>(), ctx->ws.as<uint32_t>(64),
+                             (uint32_t)ctx->n_cu, s));
     return leave(ctx, s, cap, rc);
 }
 
@@ -659,6 +687,22 @@ int fetch_out(const crdt_awset_out* h, const crdt_awset_out& d, uint32_t n_docs,
 }  // namespace
 
 extern "C" {
+
+int crdt_awset_sort_batch(crdt_ctx* ctx, const crdt_awset_batch* in, const crdt_awset_out* out) {
+    if (!ctx || !in || !in->offsets || !out_ptrs_ok(out) || in->R == 0 || in->R > CRDT_MAX_R) return CRDT_E_INVALID;
+    const uint32_t n = in->n_docs;
+    const size_t slots = in->offsets[n];
+    int rc = set_device(ctx);
+    if (rc != CRDT_OK) return rc;
+    Stager st{ctx};
+    crdt_awset_batch di = stage_batch(st, in);
+    crdt_awset_out dout = stage_out(st, n, in->R, slots);
+    if (st.rc != CRDT_OK) return st.rc;
+    rc = crdt_awset_sort_async(ctx, &di, (uint32_t)slots, &dout, ctx->stream);
+    if (rc == CRDT_OK) rc = fetch_out(out, dout, n, in->R, slots, ctx->stream);
+    const int sync = crdt_ctx_sync(ctx, ctx->stream);
+    return rc != CRDT_OK ? rc : sync;
+}
 
 int crdt_awset_apply_batch(crdt_ctx* ctx, const crdt_awset_batch* state, const crdt_tomb_batch* tombs,
                            const crdt_op_batch* ops, const crdt_awset_out* out, const crdt_tomb_out* tomb_out) {

@@ -19,6 +19,7 @@ constexpr uint32_t kErrActorRange = 1u;
 constexpr uint32_t kErrWorkspace = 2u;  // fold scratch smaller than the output slots
 constexpr uint32_t kErrHint = 4u;       // a doc broke the crdt_ctx_set_max_doc_entries promise
 constexpr uint32_t kErrCapacity = 8u;   // a doc's live count exceeds its slots (clamped)
+constexpr uint32_t kErrDupKey = 16u;    // a key appears twice in one document (ingest sort)
 
 // Kernel-side view of an AWSet batch (same fields as crdt_awset_batch).
 struct BatchView {

@@ -85,6 +85,7 @@ extern "C" {
 #define CRDT_E_NOMEM (-6)       /* device allocation failed                            */
 #define CRDT_E_WORKSPACE (-7)   /* fold block path needs crdt_ctx_reserve(max_fold_slots) */
 #define CRDT_E_RCCL (-8)        /* RCCL not loadable, or a collective failed          */
+#define CRDT_E_DUP_KEY (-9)     /* a key appears twice in one document (ingest sort)  */
 
 #define CRDT_MAX_R 64 /* version-vector length limit (one wave lane per actor) */
 
@@ -263,6 +264,17 @@ int crdt_awset_apply_async(crdt_ctx* ctx, const crdt_awset_batch* state, const c
                            void* stream);
 int crdt_awset_apply_batch(crdt_ctx* ctx, const crdt_awset_batch* state, const crdt_tomb_batch* tombs,
                            const crdt_op_batch* ops, const crdt_awset_out* out, const crdt_tomb_out* tomb_out);
+
+/* ---- ingest sort ---------------------------------------------------------
+ * The merge kernels need each document's keys strictly ascending; a producer
+ * that packs Go maps (random iteration order) can hand them over unsorted and
+ * sort on the device: out gets each document's live entries ordered by key, at
+ * the same slot offsets as `in` (out must not alias in; capacity = in's
+ * slots), counts = live counts, VVs copied.  A key twice in one document:
+ * CRDT_E_DUP_KEY.  n_slots = in->offsets[n_docs] (host-known for async). */
+int crdt_awset_sort_async(crdt_ctx* ctx, const crdt_awset_batch* in, uint32_t n_slots, const crdt_awset_out* out,
+                          void* stream);
+int crdt_awset_sort_batch(crdt_ctx* ctx, const crdt_awset_batch* in, const crdt_awset_out* out);
 
 /* ---- opt-in tombstone GC -------------------------------
  * The reference never collects tombstones: (*AWSetDelta).gcDeleted is an

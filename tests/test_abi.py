@@ -23,7 +23,7 @@ def test_exports_every_header_symbol():
 
 def test_abi_version_and_strerror():
     assert crdtgpu.lib().crdt_abi_version() == 1
-    for code in (0, -1, -2, -3, -4, -5, -6, -7, -8):
+    for code in (0, -1, -2, -3, -4, -5, -6, -7, -8, -9):
         assert crdtgpu.strerror(code) != "unknown error"
     assert "panic" in crdtgpu.strerror(crdtgpu.CRDT_E_ACTOR_RANGE)
 
