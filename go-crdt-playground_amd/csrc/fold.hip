@@ -51,9 +51,15 @@ namespace crdt {
 //             store is issued unconditionally (out-of-range offsets where there
 //             is nothing to write), so the count of memory operations after the
 //             next document's prefetch is fixed and its wait is an exact vmcnt.
+#ifndef CRDT_FOLD_WPE
+#define CRDT_FOLD_WPE 3  // waves per SIMD the fold kernel is compiled for
+#endif
+#ifndef CRDT_FOLD_VCAP
+#define CRDT_FOLD_VCAP 256
+#endif
 struct FoldSmem {
     static constexpr int NCAP = 256;  // document entries + source entries + tombstones
-    static constexpr int VCAP = 256;  // sources x R clock words
+    static constexpr int VCAP = CRDT_FOLD_VCAP;  // sources x R clock words
     static constexpr int MCAP = 64;   // sources per document
     uint64_t tk[NCAP];        // tuple keys; compacted kept keys; after the sort: segment keys
     uint64_t tc[NCAP];        // tuple counters
@@ -65,6 +71,7 @@ struct FoldSmem {
     uint16_t stag[NCAP];      // kept tuples' tags
     uint8_t anye[MCAP];       // step j has a changed entry
     uint8_t anyt[MCAP];       // step j has an effective tombstone
+    alignas(4) uint8_t smark[NCAP];  // s + 1 where source s's entries / tombstones end (step of a tuple)
 };
 
 // Tuple tag: bits 15..8 = 0 for a document entry, (j+1)*2 for an entry of
@@ -234,7 +241,7 @@ constexpr int kFoldK = 32;     // consecutive documents per wavefront
 constexpr int kFoldStores = 4 * 3 + 2;  // stores of one document's write-out (walk rounds x 3 + count + VV)
 
 template <int K, bool DELTA>
-__global__ __launch_bounds__(kFoldWaves * 64) __attribute__((amdgpu_waves_per_eu(3))) void fold_pipe_kernel(BatchView dst, SrcView sb, OutView out, Work wk) {
+__global__ __launch_bounds__(kFoldWaves * 64) __attribute__((amdgpu_waves_per_eu(CRDT_FOLD_WPE))) void fold_pipe_kernel(BatchView dst, SrcView sb, OutView out, Work wk) {
     using Smem = FoldSmem;
     __shared__ Smem smem[kFoldWaves];
     const uint32_t lane = threadIdx.x & 63;
@@ -372,6 +379,16 @@ __global__ __launch_bounds__(kFoldWaves * 64) __attribute__((amdgpu_waves_per_eu
                 m.anye[lane] = 0;
                 m.anyt[lane] = 0;
             }
+            reinterpret_cast<uint32_t*>(m.smark)[lane] = 0u;
+            wave_sync();
+            // Source s's tuples end at soffv / toffv (nondecreasing in s): mark
+            // s + 1 at that position (the last source ending there), so a tuple's
+            // step is the largest mark at or before it within its region.
+            const uint32_t nse = (uint32_t)__shfl_down((int)soffv, 1), nte = (uint32_t)__shfl_down((int)toffv, 1);
+            const bool lasts = lane + 1u == cur.ms;
+            if (lane < cur.ms && soffv < cur.E && (lasts || nse != soffv)) m.smark[cur.n + soffv] = (uint8_t)(lane + 1u);
+            if (lane < cur.ms && toffv < cur.X && (lasts || nte != toffv))
+                m.smark[cur.n + cur.E + toffv] = (uint8_t)(lane + 1u);
             vreg = P.dv;
         }
         wave_sync();
@@ -381,6 +398,7 @@ __global__ __launch_bounds__(kFoldWaves * 64) __attribute__((amdgpu_waves_per_eu
         nxt.big = 1u;
         if (k + 1 < cnt) {
             nxt = meta(k + 1);
+            STAMP(12)
             if (!nxt.big) prefetch(P, nxt);
         }
         STAMP(1)
@@ -393,11 +411,22 @@ __global__ __launch_bounds__(kFoldWaves * 64) __attribute__((amdgpu_waves_per_eu
             const uint32_t n = cur.n, E = cur.E, N = cur.N, ms = cur.ms;
             // schedule: U_j, one lane per actor
             uint64_t v = vreg;
-            for (uint32_t j = 0; j < ms; ++j) {
-                if (lane < R) {
+            uint32_t j = 0;
+            if (lane < R) {
+                for (; j + 4u <= ms; j += 4u) {  // four clock loads in flight per round
+                    uint64_t sw[4];
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) sw[u] = m.svv[(j + u) * R + lane];
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        m.vs[(j + u) * R + lane] = v;
+                        v = v > sw[u] ? v : sw[u];
+                    }
+                }
+                for (; j < ms; ++j) {
                     m.vs[j * R + lane] = v;
-                    const uint64_t s = m.svv[j * R + lane];
-                    v = v > s ? v : s;
+                    const uint64_t sw = m.svv[j * R + lane];
+                    v = v > sw ? v : sw;
                 }
             }
             vfin = v;
@@ -414,24 +443,40 @@ __global__ __launch_bounds__(kFoldWaves * 64) __attribute__((amdgpu_waves_per_eu
             STAMP(2)
             // classify the tuples: kind, step, changed / effective
             const uint32_t NQ = (N + 63u) >> 6;
-            uint32_t step[4], rel[4];
+            uint32_t step[4];
             bool isE[4], isT[4];
 #pragma unroll
             for (int c = 0; c < 4; ++c) {
                 const uint32_t i = c * 64u + lane;
                 isE[c] = i >= n && i < n + E;
                 isT[c] = i >= n + E && i < N;
-                rel[c] = isE[c] ? i - n : i - n - E;
                 step[c] = 0;
             }
-            // step of a source tuple = number of sources whose range ends at or before it
-            const uint32_t c0 = n >> 6;  // first chunk holding a source tuple
-            for (uint32_t s = 0; s < ms; ++s) {
-                const uint32_t se = rl(soffv, s), te = rl(toffv, s);
+            // step of a source tuple = number of sources whose range ends at or
+            // before it = the largest mark at or before it in its region: a max-scan
+            // of (region << 8 | mark) (regions ascend, so the scan never looks back
+            // into an earlier region's marks)
+            {
+                const uint32_t c0 = n >> 6;  // first chunk holding a source tuple
+                uint32_t carry = 0;
 #pragma unroll
-                for (int c = 0; c < 4; ++c)
-                    if ((uint32_t)c >= c0 && (uint32_t)c < NQ) step[c] += rel[c] >= (isE[c] ? se : te) ? 1u : 0u;
+                for (int c = 0; c < 4; ++c) {
+                    if ((uint32_t)c >= c0 && (uint32_t)c < NQ) {
+                        const uint32_t i = c * 64u + lane;
+                        uint32_t x = ((isT[c] ? 2u : (isE[c] ? 1u : 0u)) << 8) | m.smark[i];
+                        x = max(x, dpp<0x111>(0u, x));         // row_shr:1
+                        x = max(x, dpp<0x112>(0u, x));         // row_shr:2
+                        x = max(x, dpp<0x114>(0u, x));         // row_shr:4
+                        x = max(x, dpp<0x118>(0u, x));         // row_shr:8
+                        x = max(x, dpp<0x142, 0xA>(0u, x));    // row_bcast:15
+                        x = max(x, dpp<0x143, 0xC>(0u, x));    // row_bcast:31
+                        x = max(x, carry);
+                        carry = (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
+                        step[c] = x & 0xFFu;
+                    }
+                }
             }
+            STAMP(10)
             uint32_t cmax = 0;  // longest source: depth of the re-add search
             if (DELTA && cur.X) {
                 const uint32_t prv = (uint32_t)__shfl_up((int)soffv, 1);
@@ -439,6 +484,7 @@ __global__ __launch_bounds__(kFoldWaves * 64) __attribute__((amdgpu_waves_per_eu
 #pragma unroll
                 for (int o = 32; o > 0; o >>= 1) cmax = max(cmax, (uint32_t)__shfl_xor((int)cmax, o));
             }
+            STAMP(11)
             uint64_t key[4];
             uint32_t flag = 0, perr = 0;  // flag bit c: changed entry / effective tombstone
 #pragma unroll
