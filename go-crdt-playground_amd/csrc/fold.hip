@@ -338,8 +338,10 @@ __global__ __launch_bounds__(kFoldWaves * 64) __attribute__((amdgpu_waves_per_eu
 
     FoldPref P;
     P.eo2 = P.to = P.to2 = 0;
-    DocMeta cur = meta(0);
-    if (!cur.big) prefetch(P, cur);
+    {
+        const DocMeta q0 = meta(0);
+        if (!q0.big) prefetch(P, q0);
+    }
     {   // As many (out-of-range, no-traffic) stores as a document's write-out
         // issues, so the loop is entered with the same memory operations
         // behind the prefetch as every later iteration: the compiler's vmcnt
@@ -351,6 +353,9 @@ __global__ __launch_bounds__(kFoldWaves * 64) __attribute__((amdgpu_waves_per_eu
 #pragma unroll 1
     for (uint32_t k = 0; k < cnt; ++k) {
         STAMP(15)
+        // metadata re-read per document (lane k of the run's vectors), not carried
+        // across the fold: fewer scalar registers live through the loop body
+        const DocMeta cur = meta(k);
         // ---- stage document k (its loads were issued one document ago)
         uint64_t vreg = 0;              // lane r < R: V_0[r]
         uint32_t soffv = 0, toffv = 0;  // lane s: end of source s's entries / tombstones
@@ -366,12 +371,12 @@ __global__ __launch_bounds__(kFoldWaves * 64) __attribute__((amdgpu_waves_per_eu
                 }
                 if ((uint32_t)c * 64u < msR && i < msR) m.svv[i] = P.sv[c];
             }
-            const uint32_t nso = lane == 63 ? rl(P.eo2, 0) : (uint32_t)__shfl_down((int)P.eo, 1);
+            const uint32_t nso = from_next_lane(rl(P.eo2, 0), P.eo);
             soffv = nso - cur.e0;
             if (lane <= cur.ms) m.soff[lane] = P.eo - cur.e0;
             if (lane == 0 && cur.ms >= 64) m.soff[64] = P.eo2 - cur.e0;
             if (tombs) {
-                const uint32_t nto = lane == 63 ? rl(P.to2, 0) : (uint32_t)__shfl_down((int)P.to, 1);
+                const uint32_t nto = from_next_lane(rl(P.to2, 0), P.to);
                 toffv = nto - cur.t0;
             }
             if (lane < cur.ms) {
@@ -384,7 +389,7 @@ __global__ __launch_bounds__(kFoldWaves * 64) __attribute__((amdgpu_waves_per_eu
             // Source s's tuples end at soffv / toffv (nondecreasing in s): mark
             // s + 1 at that position (the last source ending there), so a tuple's
             // step is the largest mark at or before it within its region.
-            const uint32_t nse = (uint32_t)__shfl_down((int)soffv, 1), nte = (uint32_t)__shfl_down((int)toffv, 1);
+            const uint32_t nse = from_next_lane(0u, soffv), nte = from_next_lane(0u, toffv);
             const bool lasts = lane + 1u == cur.ms;
             if (lane < cur.ms && soffv < cur.E && (lasts || nse != soffv)) m.smark[cur.n + soffv] = (uint8_t)(lane + 1u);
             if (lane < cur.ms && toffv < cur.X && (lasts || nte != toffv))
@@ -394,10 +399,8 @@ __global__ __launch_bounds__(kFoldWaves * 64) __attribute__((amdgpu_waves_per_eu
         wave_sync();
         STAMP(0)
         // ---- issue document k+1's loads; they fly while document k is folded
-        DocMeta nxt = cur;
-        nxt.big = 1u;
         if (k + 1 < cnt) {
-            nxt = meta(k + 1);
+            const DocMeta nxt = meta(k + 1);
             STAMP(12)
             if (!nxt.big) prefetch(P, nxt);
         }
@@ -479,10 +482,15 @@ __global__ __launch_bounds__(kFoldWaves * 64) __attribute__((amdgpu_waves_per_eu
             STAMP(10)
             uint32_t cmax = 0;  // longest source: depth of the re-add search
             if (DELTA && cur.X) {
-                const uint32_t prv = (uint32_t)__shfl_up((int)soffv, 1);
+                const uint32_t prv = dpp<0x138>(0u, soffv);  // wave_shr:1
                 cmax = lane < ms ? soffv - (lane ? prv : 0u) : 0u;
-#pragma unroll
-                for (int o = 32; o > 0; o >>= 1) cmax = max(cmax, (uint32_t)__shfl_xor((int)cmax, o));
+                cmax = max(cmax, dpp<0x111>(0u, cmax));  // inclusive max-scan (DPP, no LDS) ...
+                cmax = max(cmax, dpp<0x112>(0u, cmax));
+                cmax = max(cmax, dpp<0x114>(0u, cmax));
+                cmax = max(cmax, dpp<0x118>(0u, cmax));
+                cmax = max(cmax, dpp<0x142, 0xA>(0u, cmax));
+                cmax = max(cmax, dpp<0x143, 0xC>(0u, cmax));
+                cmax = (uint32_t)__builtin_amdgcn_readlane((int)cmax, 63);  // ... whose last lane has the maximum
             }
             STAMP(11)
             uint64_t key[4];
@@ -628,7 +636,6 @@ __global__ __launch_bounds__(kFoldWaves * 64) __attribute__((amdgpu_waves_per_eu
         st64(vfin, make_rsrc(out.vv + (size_t)cur.d * R, cur.big ? 0u : R * 8u), lane * 8u);
         wave_sync();
         STAMP(6)
-        cur = nxt;
     }
     STAMP_FLUSH
     flag_error(wk.status, err);
