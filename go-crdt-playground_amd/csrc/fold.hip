@@ -51,15 +51,19 @@ namespace crdt {
 //             store is issued unconditionally (out-of-range offsets where there
 //             is nothing to write), so the count of memory operations after the
 //             next document's prefetch is fixed and its wait is an exact vmcnt.
-#ifndef CRDT_FOLD_WPE
-#define CRDT_FOLD_WPE 3  // waves per SIMD the fold kernel is compiled for
-#endif
-#ifndef CRDT_FOLD_VCAP
-#define CRDT_FOLD_VCAP 256
-#endif
+// Waves per SIMD: the delta fold needs 168 VGPRs (3 waves); the AWSet fold
+// fits 128 (4 waves), which also needs its LDS trimmed to 16 waves per CU
+// (160 KiB): 224 clock words per document instead of 256.
+template <bool DELTA>
+struct FoldShape {
+    static constexpr int WPE = DELTA ? 3 : 4;
+    static constexpr int VCAP = DELTA ? 256 : 224;
+};
+
+template <int VCAP_>
 struct FoldSmem {
     static constexpr int NCAP = 256;  // document entries + source entries + tombstones
-    static constexpr int VCAP = CRDT_FOLD_VCAP;  // sources x R clock words
+    static constexpr int VCAP = VCAP_;  // sources x R clock words
     static constexpr int MCAP = 64;   // sources per document
     uint64_t tk[NCAP];        // tuple keys; compacted kept keys; after the sort: segment keys
     uint64_t tc[NCAP];        // tuple counters
@@ -101,8 +105,8 @@ struct Emit {
 // The current dot is the last entry's, whatever the presence, so it is one
 // segmented scan; with the gap folded in, each tuple is again constant or
 // identity, and the final presence is the last constant: a second scan.
-template <int EPL, bool DELTA>
-__device__ __forceinline__ uint32_t sort_resolve(const FoldSmem& m, uint32_t Kc, uint32_t ms, uint32_t R,
+template <int EPL, bool DELTA, class Smem>
+__device__ __forceinline__ uint32_t sort_resolve(const Smem& m, uint32_t Kc, uint32_t ms, uint32_t R,
                                                  uint64_t full_mask, uint32_t lane, uint64_t lt, Emit& e,
                                                  uint32_t& err STAMP_PARAM) {
     uint64_t k[EPL];
@@ -241,8 +245,8 @@ constexpr int kFoldK = 32;     // consecutive documents per wavefront
 constexpr int kFoldStores = 4 * 3 + 2;  // stores of one document's write-out (walk rounds x 3 + count + VV)
 
 template <int K, bool DELTA>
-__global__ __launch_bounds__(kFoldWaves * 64) __attribute__((amdgpu_waves_per_eu(CRDT_FOLD_WPE))) void fold_pipe_kernel(BatchView dst, SrcView sb, OutView out, Work wk) {
-    using Smem = FoldSmem;
+__global__ __launch_bounds__(kFoldWaves * 64) __attribute__((amdgpu_waves_per_eu(FoldShape<DELTA>::WPE))) void fold_pipe_kernel(BatchView dst, SrcView sb, OutView out, Work wk) {
+    using Smem = FoldSmem<FoldShape<DELTA>::VCAP>;
     __shared__ Smem smem[kFoldWaves];
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t w = threadIdx.x >> 6;
