@@ -54,10 +54,13 @@ namespace crdt {
 // Waves per SIMD: the delta fold needs 168 VGPRs (3 waves); the AWSet fold
 // fits 128 (4 waves), which also needs its LDS trimmed to 16 waves per CU
 // (160 KiB): 224 clock words per document instead of 256.
+#ifndef CRDT_FOLD_DELTA_WPE
+#define CRDT_FOLD_DELTA_WPE 3  // probe builds may override (tools/fold_probe.hip)
+#endif
 template <bool DELTA>
 struct FoldShape {
-    static constexpr int WPE = DELTA ? 3 : 4;
-    static constexpr int VCAP = DELTA ? 256 : 224;
+    static constexpr int WPE = DELTA ? CRDT_FOLD_DELTA_WPE : 4;
+    static constexpr int VCAP = (DELTA && CRDT_FOLD_DELTA_WPE < 4) ? 256 : 224;
 };
 
 template <int VCAP_>
