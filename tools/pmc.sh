@@ -27,7 +27,7 @@ if [ "${FOLD:-0}" = 1 ]; then
   pass write WRITE_SIZE
   cpass calib_fetch FETCH_SIZE
   cpass calib_write WRITE_SIZE
-  python3 tools/traffic.py "$OUT" --docs ${DOCS:-1048576} --config ${CONFIG:-3} --kernel ${KERNEL:-fold_pipe_kernel} --emit > "$OUT/summary.txt"; cat "$OUT/summary.txt"
+  python3 tools/traffic.py "$OUT" --docs ${DOCS:-1048576} --config ${CONFIG:-3} --kernel "${KERNEL:-fold_pipe_kernel}" --emit > "$OUT/summary.txt"; cat "$OUT/summary.txt"
   exit 0
 fi
 pass fetch FETCH_SIZE

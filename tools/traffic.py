@@ -63,7 +63,7 @@ def main():
     wcorr = (8 * N) / (cal["WRITE_SIZE"] * 1024) if cal.get("WRITE_SIZE") else None
     jk = next((k for k in out if k.startswith(a.kernel)), "")
     j = out.get(jk, {})
-    res = {"docs": a.docs, "config": a.config, "kernel": jk, "exchange": jk.endswith("true>"),
+    res = {"docs": a.docs, "config": a.config, "kernel": jk, "exchange": jk.startswith("join") and jk.endswith("true>"),
            "fetch_correction": fcorr, "write_correction": wcorr}
     if j.get("FETCH_SIZE") is not None and j.get("WRITE_SIZE") is not None:
         rd = j["FETCH_SIZE"] * 1024 * (fcorr or 1.0)
