@@ -28,9 +28,17 @@ __global__ __launch_bounds__(NT) void context_partial_kernel(const uint64_t* __r
     uint64_t m = 0;
     if (lane_doc < per) {
         const size_t stride = (size_t)gridDim.x * per;
-        for (size_t d = (size_t)blockIdx.x * per + lane_doc; d < n_docs; d += stride) {
-            const uint64_t v = vv[d * R + r];
-            m = v > m ? v : m;
+        // eight independent loads in flight per round (a plain strided loop
+        // waits out one HBM latency per document)
+        for (size_t d0 = (size_t)blockIdx.x * per + lane_doc; d0 < n_docs; d0 += 8 * stride) {
+            uint64_t v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const size_t d = d0 + u * stride;
+                v[u] = d < n_docs ? vv[d * R + r] : 0ull;
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) m = v[u] > m ? v[u] : m;
         }
     }
     red[t] = m;
@@ -56,9 +64,15 @@ __global__ __launch_bounds__(NT) void context_final_kernel(const uint64_t* __res
     const uint32_t r = t % R, row = t / R;
     uint64_t m = 0;
     if (row < per)
-        for (uint32_t b = row; b < n_part; b += per) {
-            const uint64_t v = part[(size_t)b * R + r];
-            m = v > m ? v : m;
+        for (uint32_t b0 = row; b0 < n_part; b0 += 8 * per) {
+            uint64_t v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const uint32_t b = b0 + u * per;
+                v[u] = b < n_part ? part[(size_t)b * R + r] : 0ull;
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) m = v[u] > m ? v[u] : m;
         }
     red[t] = m;
     __syncthreads();
