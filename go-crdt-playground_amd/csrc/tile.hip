@@ -30,6 +30,7 @@
 // dot differs, the src dot wins (awset.go:142), so each survivor stages two
 // LDS indices: the dot for out1 and the dot for out2.
 #include "crdt_device.hpp"
+#include "wave_sort.hpp"
 #include "merge_block.hpp"
 
 namespace crdt {
@@ -174,9 +175,13 @@ __device__ __forceinline__ uint32_t look_back(uint64_t* flags, uint32_t g, uint3
             continue;
         }
         uint32_t v = lane <= first_inc ? (uint32_t)f : 0u;
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) v += (uint32_t)__shfl_xor((int)v, o);
-        prefix += v;
+        v += dpp<0x111>(0u, v);  // wave sum: DPP inclusive scan (no LDS round trips) ...
+        v += dpp<0x112>(0u, v);
+        v += dpp<0x114>(0u, v);
+        v += dpp<0x118>(0u, v);
+        v += dpp<0x142, 0xA>(0u, v);
+        v += dpp<0x143, 0xC>(0u, v);
+        prefix += (uint32_t)__builtin_amdgcn_readlane((int)v, 63);  // ... whose last lane holds the total
         if (first_inc < 64u) break;
         look -= 64;
         rem -= 64;
