@@ -13,6 +13,7 @@ restatement, so a pass here says the formulation is the reference's
 semantics, including which HasDot calls can panic; the GPU tests then check
 the kernel against the same oracle."""
 
+import itertools
 import random
 
 import pytest
@@ -227,3 +228,54 @@ def test_per_key_model_matches_oracle(mode, seed):
         assert vv == want.vv[:R].tolist()
         checked += 1
     assert checked > 50 and errs > 0
+
+
+def kernel_steps(n, ent_sizes, tomb_sizes):
+    """The fold kernel's step-of-tuple (csrc/fold.hip, fold_pipe_kernel): lane s
+    marks s + 1 where source s's entries / tombstones end (only the last source
+    ending at a position writes), then a max-scan of (region << 8 | mark) over
+    the tuple positions, 64 per chunk with the previous chunk's last lane
+    carried (the DPP row_shr / row_bcast scan is a plain prefix max here)."""
+    ms = len(ent_sizes)
+    E, X = sum(ent_sizes), sum(tomb_sizes)
+    N = n + E + X
+    mark = [0] * 256
+    soff = list(itertools.accumulate(ent_sizes))  # lane s: end of source s's entries
+    toff = list(itertools.accumulate(tomb_sizes))
+    for s in range(ms):
+        last = s + 1 == ms
+        if soff[s] < E and (last or soff[s + 1] != soff[s]):
+            mark[n + soff[s]] = s + 1
+        if toff[s] < X and (last or toff[s + 1] != toff[s]):
+            mark[n + E + toff[s]] = s + 1
+    steps, carry = [], 0
+    for c in range((N + 63) // 64):
+        run = carry
+        for lane in range(64):
+            i = c * 64 + lane
+            region = 2 if n + E <= i < N else (1 if n <= i < n + E else 0)
+            run = max(run, (region << 8) | mark[i])
+            if i < N:
+                steps.append(run & 0xFF)
+        carry = run
+    return steps
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_step_of_tuple_marks(seed):
+    """Every source tuple gets the index of the source holding it, empty sources
+    (shared end positions) included; document entries get 0."""
+    rng = random.Random(seed)
+    for _ in range(300):
+        ms = rng.randint(1, 64)
+        n = rng.randint(0, 64)
+        ent = [rng.choice([0, 0, 1, 2, 3, 8]) for _ in range(ms)]
+        tomb = [rng.choice([0, 0, 0, 1, 2]) for _ in range(ms)]
+        if n + sum(ent) + sum(tomb) > 256:
+            continue
+        want = [0] * n
+        for s, k in enumerate(ent):
+            want += [s] * k
+        for s, k in enumerate(tomb):
+            want += [s] * k
+        assert kernel_steps(n, ent, tomb) == want
