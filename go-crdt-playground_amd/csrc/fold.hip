@@ -655,6 +655,7 @@ __global__ __launch_bounds__(NT) void fold_block_kernel(int mode, BatchView dst,
     const uint32_t tid = threadIdx.x;
     const uint32_t R = dst.R;
     uint32_t err = 0;
+    if (work_total(wk, dst.n_docs) == 0) return;  // empty worklist (set by the previous launch): no dispensing atomics
     for (;;) {
         if (tid == 0) sm.word[0] = atomicAdd(wk.wl_head, 1u);
         __syncthreads();

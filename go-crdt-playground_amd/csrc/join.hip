@@ -236,6 +236,7 @@ __global__ __launch_bounds__(NT) void join_block_kernel(BatchView dst, BatchView
     const uint32_t R = dst.R;
     uint32_t err = 0;
     const Entries none{nullptr, nullptr, nullptr, 0};
+    if (work_total(wk, dst.n_docs) == 0) return;  // empty worklist (set by the previous launch): no dispensing atomics
     for (;;) {
         if (tid == 0) sm.word[0] = atomicAdd(wk.wl_head + head, 1u);
         __syncthreads();
