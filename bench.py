@@ -40,6 +40,30 @@ sys.path.insert(0, os.path.join(ROOT, "go-crdt-playground_amd"))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level table)
+COPY_MEASURED_GBS = 6290.0  # float4 copy measured on MI355X (MI355X_MICROARCH.md; SURVEY.md 8d second denominator)
+
+
+def box_probe(eng, dev, nbytes=2 << 30, reps=20):
+    """This box's own HBM ceiling, measured before any timing (crdt_bw_probe):
+    streaming read, non-temporal write and copy over 2 GiB buffers (8x the
+    256 MiB Infinity Cache), GB/s.  Boxes of one pool differ, so
+    the line states the ceiling of the box that produced it."""
+    import torch
+
+    from crdtgpu import abi
+
+    a = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    b = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    a.fill_(0x5A)
+    torch.cuda.synchronize()
+    out = {"bytes": nbytes, "reps": reps,
+           "read_gbs": eng.bw_probe(abi.CRDT_PROBE_READ, a, b, nbytes, reps),
+           "write_gbs": eng.bw_probe(abi.CRDT_PROBE_WRITE, None, b, nbytes, reps),
+           "copy_gbs": eng.bw_probe(abi.CRDT_PROBE_COPY, a, b, nbytes, reps)}
+    del a, b
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    return out
 
 
 def _np_copy(t, n, dt):
@@ -428,7 +452,18 @@ def _traffic(path, config, n, W):
     return None
 
 
-def run_config(config, n, args, ctx, steps, warmup, repeats, cpu):
+def _box_fields(roof, box):
+    """frac against this box's measured copy ceiling and against SURVEY 8d's 6.29 TB/s."""
+    a = roof["achieved"]
+    roof["frac_vs_6290"] = a / COPY_MEASURED_GBS
+    if box:
+        roof["box_read_gbs"] = box["read_gbs"]
+        roof["box_write_gbs"] = box["write_gbs"]
+        roof["box_copy_gbs"] = box["copy_gbs"]
+        roof["frac_vs_box"] = a / box["copy_gbs"] if box["copy_gbs"] else None
+
+
+def run_config(config, n, args, ctx, steps, warmup, repeats, cpu, box=None):
     """Build one workload, time it, and return its result dict (the bench line's
     fields).  Inputs are generated on the device before any timing."""
     import numpy as np
@@ -546,6 +581,7 @@ def run_config(config, n, args, ctx, steps, warmup, repeats, cpu):
         "replay_check": replay_check,
         "global_causal_context": g.cpu().numpy().view(np.uint64).tolist() if g is not None else [],
     }
+    _box_fields(res["roofline"], box)
     if per_merge_bytes != bytes_launch:
         res["roofline"]["survey_8d_per_merge_bytes"] = per_merge_bytes
     if graph_error:
@@ -605,6 +641,7 @@ def main():
     ap.add_argument("--separate", action="store_true", help="configs 2/4: two join launches instead of one exchange")
     ap.add_argument("--no-graph", action="store_true", help="launch eagerly instead of replaying a captured HIP graph")
     ap.add_argument("--no-boundary", action="store_true", help="skip the host boundary-cost leg")
+    ap.add_argument("--no-box-probe", action="store_true", help="skip the box bandwidth probes")
     ap.add_argument("--boundary-docs", type=int, default=65536)
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
     args = ap.parse_args()
@@ -643,8 +680,9 @@ def main():
     else:
         legs = [int(x) for x in args.legs.split(",") if x and int(x) != args.config]
 
+    box = None if args.no_box_probe else box_probe(eng, dev)
     n = args.docs or DEFAULT_DOCS[args.config]
-    head = run_config(args.config, n, args, ctx, args.steps, args.warmup, args.repeats, not args.no_cpu_baseline)
+    head = run_config(args.config, n, args, ctx, args.steps, args.warmup, args.repeats, not args.no_cpu_baseline, box)
     result = {
         "metric": head.pop("metric"),
         "value": head.pop("value"),
@@ -660,11 +698,15 @@ def main():
         "data": "synthetic (AWSet states generated on device, csrc/gen.hip)",
     }
     result.update(head)
+    if box:
+        result["box_probe"] = dict(box, what="crdt_bw_probe on this box before timing: streaming read (16 B/lane), "
+                                             "non-temporal write, copy (read+write bytes); roofline.frac_vs_box = "
+                                             "achieved / copy_gbs")
     if legs:
         result["legs"] = {}
         for c in legs:
             result["legs"]["config%d" % c] = run_config(c, DEFAULT_DOCS[c], args, ctx, args.leg_steps,
-                                                        args.leg_warmup, 1, not args.no_cpu_baseline)
+                                                        args.leg_warmup, 1, not args.no_cpu_baseline, box)
     if rank == 0 and world == 1 and not args.no_boundary:
         result["boundary"] = boundary_cost(args.boundary_docs)
     if rank == 0:

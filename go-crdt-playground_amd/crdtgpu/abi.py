@@ -34,6 +34,9 @@ CRDT_OP_DEL = 1
 CRDT_OP_DELTA_DEL = 2
 CRDT_OP_DELTA_DEL_KEY = 3
 CRDT_MAX_OPS_PER_DOC = 256
+CRDT_PROBE_READ = 0
+CRDT_PROBE_WRITE = 1
+CRDT_PROBE_COPY = 2
 
 _vp = ctypes.c_void_p
 _u32 = ctypes.c_uint32
@@ -140,8 +143,11 @@ def _load():
         "crdt_gen_replicas_async": (ctypes.c_int, [_vp, _u64, _u32, _u32, _u32, P(CAWSetOut), P(CSrcBatch), _vp]),
         "crdt_awset_join_batch": (ctypes.c_int, [_vp, P(CAWSetBatch), P(CAWSetBatch), P(CAWSetOut)]),
         "crdt_awset_fold_batch": (ctypes.c_int, [_vp, ctypes.c_int, P(CAWSetBatch), P(CSrcBatch), P(CAWSetOut)]),
+        "crdt_bw_probe": (ctypes.c_int, [_vp, ctypes.c_int, _vp, _vp, ctypes.c_size_t, ctypes.c_int,
+                                         P(ctypes.c_double)]),
         "crdt_validate_batch": (ctypes.c_int, [P(CAWSetBatch)]),
         "crdt_validate_src_batch": (ctypes.c_int, [P(CSrcBatch)]),
+        "crdt_validate_tomb_batch": (ctypes.c_int, [P(CTombBatch), _u32]),
         "crdt_awset_apply_async": (ctypes.c_int, [_vp, P(CAWSetBatch), P(CTombBatch), P(COpBatch), P(CAWSetOut),
                                                   P(CTombOut), _vp]),
         "crdt_awset_apply_batch": (ctypes.c_int, [_vp, P(CAWSetBatch), P(CTombBatch), P(COpBatch), P(CAWSetOut),

@@ -61,6 +61,14 @@ class Engine:
     def sync(self, stream=None):
         check(self._lib.crdt_ctx_sync(self._ctx, _stream(stream)), "crdt_ctx_sync")
 
+    def bw_probe(self, kind: int, a, b, nbytes: int, reps: int = 10) -> float:
+        """GB/s of a streaming read / write / copy over device buffers a, b (crdt_bw_probe)."""
+        g = ctypes.c_double()
+        pa = a.data_ptr() if a is not None else None
+        check(self._lib.crdt_bw_probe(self._ctx, int(kind), pa, b.data_ptr(), int(nbytes), int(reps), ctypes.byref(g)),
+              "crdt_bw_probe")
+        return g.value
+
     # -- device-resident, asynchronous -------------------------------------
     def join_async(self, dst: AWSetBatch, src: AWSetBatch, out: OutBuffers, stream=None):
         d, s, o = _c(dst), _c(src), _c(out)
@@ -273,3 +281,8 @@ def validate(batch: AWSetBatch) -> int:
 def validate_src(srcs: SrcBatch) -> int:
     s = srcs.numpy().c()
     return abi.lib().crdt_validate_src_batch(ctypes.byref(s))
+
+
+def validate_tombs(tombs, n_docs: int) -> int:
+    t = tombs.numpy().c()
+    return abi.lib().crdt_validate_tomb_batch(ctypes.byref(t), n_docs)

@@ -51,6 +51,7 @@ hipError_t launch_gen_replicas(uint64_t seed, uint32_t n_docs, uint32_t P, uint3
 hipError_t launch_gen_zipf(uint64_t seed, uint32_t n_docs, const uint32_t* offsets, const OutView& A,
                            const OutView& B, hipStream_t stream);
 uint32_t host_zipf_doc_size(uint64_t seed, uint32_t d);
+hipError_t launch_probe(int kind, const void* a, void* b, size_t n16, uint32_t n_cu, hipStream_t stream);
 }  // namespace crdt
 
 using namespace crdt;
@@ -279,9 +280,11 @@ int crdt_ctx_create(int device, crdt_ctx** out) {
 void crdt_ctx_destroy(crdt_ctx* ctx) {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
-    crdt_internal_comm_release(ctx);
+    // drain every queued call (an all-reduce on the communicator included)
+    // before the communicator and the workspaces go away
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     if (ctx->last_ev) (void)hipEventSynchronize(ctx->last_ev);
+    crdt_internal_comm_release(ctx);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     if (ctx->last_ev) (void)hipEventDestroy(ctx->last_ev);
     for (void* p : ctx->retired) (void)hipFree(p);
@@ -290,7 +293,9 @@ void crdt_ctx_destroy(crdt_ctx* ctx) {
     ctx->worklist.release();
     ctx->parts.release();
     ctx->scratch.release();
-    for (DevBuf* b : {&ctx->tile_desc, &ctx->tile_geo, &ctx->tile_flags, &ctx->tile_slot, &ctx->tile_run}) b->release();
+    for (DevBuf* b : {&ctx->tile_desc, &ctx->tile_geo, &ctx->tile_flags, &ctx->tile_slot, &ctx->tile_run,
+                      &ctx->sort_tmp, &ctx->sort_idx, &ctx->sort_ends})
+        b->release();
     for (auto& b : ctx->stage) b.release();
     delete ctx;
 }
@@ -580,6 +585,37 @@ int crdt_gen_zipf_async(crdt_ctx* ctx, uint64_t seed, uint32_t n_docs, const uin
     return hip_err(launch_gen_zipf(seed, n_docs, offsets, view(a), view(b), (hipStream_t)stream));
 }
 
+int crdt_bw_probe(crdt_ctx* ctx, int kind, const void* a, void* b, size_t bytes, int reps, double* gbs) {
+    if (!ctx || !gbs || kind < CRDT_PROBE_READ || kind > CRDT_PROBE_COPY || reps < 1 || bytes < 16 || !b ||
+        (kind != CRDT_PROBE_WRITE && !a))
+        return CRDT_E_INVALID;
+    int rc = set_device(ctx);
+    if (rc != CRDT_OK) return rc;
+    hipStream_t s = ctx->stream;
+    bool cap = false;
+    if ((rc = enter(ctx, s, cap)) != CRDT_OK) return rc;
+    if (cap) return CRDT_E_INVALID;
+    const size_t n16 = bytes / 16;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    rc = hip_err(hipEventCreate(&e0));
+    if (rc == CRDT_OK) rc = hip_err(hipEventCreate(&e1));
+    // one untimed launch (first touch, clocks up), then reps timed back to back
+    if (rc == CRDT_OK) rc = hip_err(launch_probe(kind, a, b, n16, (uint32_t)ctx->n_cu, s));
+    if (rc == CRDT_OK) rc = hip_err(hipEventRecord(e0, s));
+    for (int r = 0; r < reps && rc == CRDT_OK; ++r) rc = hip_err(launch_probe(kind, a, b, n16, (uint32_t)ctx->n_cu, s));
+    if (rc == CRDT_OK) rc = hip_err(hipEventRecord(e1, s));
+    if (rc == CRDT_OK) rc = hip_err(hipEventSynchronize(e1));
+    float ms = 0.f;
+    if (rc == CRDT_OK) rc = hip_err(hipEventElapsedTime(&ms, e0, e1));
+    if (e0) (void)hipEventDestroy(e0);
+    if (e1) (void)hipEventDestroy(e1);
+    if (rc == CRDT_OK) {
+        const double moved = (double)n16 * 16.0 * (kind == CRDT_PROBE_COPY ? 2.0 : 1.0);
+        *gbs = ms > 0.f ? moved * reps / (ms * 1e-3) / 1e9 : 0.0;
+    }
+    return leave(ctx, s, cap, rc);
+}
+
 /* ---------------- validation (host) ---------------- */
 
 int crdt_validate_batch(const crdt_awset_batch* b) {
@@ -614,6 +650,21 @@ int crdt_validate_src_batch(const crdt_src_batch* s) {
             for (uint32_t i = to + 1; i < te; i++)
                 if (s->tkeys[i] <= s->tkeys[i - 1]) return CRDT_E_UNSORTED;
         }
+    }
+    return CRDT_OK;
+}
+
+int crdt_validate_tomb_batch(const crdt_tomb_batch* t, uint32_t n_docs) {
+    if (!t || !t->offsets) return CRDT_E_INVALID;
+    if (n_docs && t->offsets[n_docs] > t->offsets[0] && (!t->keys || !t->actors || !t->counters))
+        return CRDT_E_INVALID;
+    for (uint32_t d = 0; d < n_docs; d++) {
+        const uint32_t o = t->offsets[d], e = t->offsets[d + 1];
+        if (e < o) return CRDT_E_INVALID;
+        const uint32_t n = t->counts ? t->counts[d] : e - o;
+        if (n > e - o) return CRDT_E_CAPACITY;
+        for (uint32_t i = o + 1; i < o + n; i++)
+            if (t->keys[i] <= t->keys[i - 1]) return CRDT_E_UNSORTED;
     }
     return CRDT_OK;
 }
@@ -711,6 +762,7 @@ int crdt_awset_apply_batch(crdt_ctx* ctx, const crdt_awset_batch* state, const c
     if (rc != CRDT_OK) return rc;
     if (ops->n_docs != state->n_docs) return CRDT_E_INVALID;
     const uint32_t n = state->n_docs;
+    if (tombs && (rc = crdt_validate_tomb_batch(tombs, n)) != CRDT_OK) return rc;
     const size_t nops = ops->op_off[n];
     if (nops && (!ops->kind || !ops->keys)) return CRDT_E_INVALID;
     const uint64_t slots = (uint64_t)state->offsets[n] + nops;

@@ -93,6 +93,17 @@ void drop_comm(const Rccl* r, crdt_ctx* c) {
     }
 }
 
+// Restores the calling thread's current HIP device on every return path.
+struct DeviceGuard {
+    int dev = -1;
+    DeviceGuard() {
+        if (hipGetDevice(&dev) != hipSuccess) dev = -1;
+    }
+    ~DeviceGuard() {
+        if (dev >= 0) (void)hipSetDevice(dev);
+    }
+};
+
 }  // namespace
 
 // Called by crdt_ctx_destroy.
@@ -116,6 +127,7 @@ int crdt_comm_unique_id(uint8_t* id) {
 
 int crdt_comm_init(crdt_ctx* ctx, int n_ranks, int rank, const uint8_t* id) {
     if (!ctx || !id || n_ranks < 1 || rank < 0 || rank >= n_ranks) return CRDT_E_INVALID;
+    DeviceGuard keep;
     const Rccl* r = rccl();
     if (!r) return CRDT_E_RCCL;
     if (hipSetDevice(crdt_internal_device(ctx)) != hipSuccess) return CRDT_E_HIP;
@@ -134,6 +146,7 @@ int crdt_context_allreduce_async(crdt_ctx* ctx, uint64_t* vv_R, uint32_t R, void
     if (!r) return CRDT_E_RCCL;
     ncclComm_t c = (ncclComm_t)*crdt_internal_comm(ctx);
     if (!c) return CRDT_E_INVALID;  // crdt_comm_init first
+    DeviceGuard keep;
     if (hipSetDevice(crdt_internal_device(ctx)) != hipSuccess) return CRDT_E_HIP;
     hipStream_t s = (hipStream_t)stream;
     int rc = crdt_internal_order(ctx, s);
@@ -144,6 +157,7 @@ int crdt_context_allreduce_async(crdt_ctx* ctx, uint64_t* vv_R, uint32_t R, void
 int crdt_global_context_allreduce(crdt_ctx* const* per_gpu, int n_gpus, uint64_t* const* vv_R, uint32_t R,
                                   uint64_t* out_vv_R) {
     if (!per_gpu || !vv_R || n_gpus < 1 || R == 0 || R > CRDT_MAX_R) return CRDT_E_INVALID;
+    DeviceGuard keep;  // the caller's current device is unchanged on return
     std::vector<int> devs(n_gpus);
     for (int i = 0; i < n_gpus; ++i) {
         if (!per_gpu[i] || !vv_R[i]) return CRDT_E_INVALID;
@@ -172,6 +186,9 @@ int crdt_global_context_allreduce(crdt_ctx* const* per_gpu, int n_gpus, uint64_t
         int rc = crdt_internal_order(per_gpu[i], crdt_internal_stream(per_gpu[i]));
         if (rc != CRDT_OK) return rc;
     }
+    // A group that was started must be ended even when an enqueue failed (an
+    // open group would swallow the caller's next RCCL calls); after the first
+    // failure no further all-reduce is enqueued and the call reports it.
     if (r->group_start() != ncclSuccess) return CRDT_E_RCCL;
     bool ok = true;
     for (int i = 0; i < n_gpus; ++i) {

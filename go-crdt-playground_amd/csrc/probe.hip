@@ -1,0 +1,62 @@
+// Bandwidth probes: what this box's HBM moves with no merge work at all.
+// Not a merge.  bench.py runs them before timing so that a bench line carries
+// the ceiling of the box it ran on next to the 8 TB/s spec figure (boxes of one
+// pool differ by up to 25 % in copy bandwidth).
+//
+//   read : 16 B per lane loads, four in flight per lane, grid-stride
+//   write: 16 B per lane non-temporal stores (the merge kernels' output stores)
+//   copy : both, one read and one write per 16 B (the merges' mixed shape)
+#include "crdt_device.hpp"
+
+namespace crdt {
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+__global__ __launch_bounds__(256) void probe_read_kernel(const u32x4* __restrict__ a, size_t n, uint32_t* sink) {
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    u32x4 acc = {0u, 0u, 0u, 0u};
+    size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    for (; i + 3 * stride < n; i += 4 * stride) {
+        const u32x4 x0 = a[i], x1 = a[i + stride], x2 = a[i + 2 * stride], x3 = a[i + 3 * stride];
+        acc ^= x0 ^ x1 ^ x2 ^ x3;
+    }
+    for (; i < n; i += stride) acc ^= a[i];
+    // never true for the probe's fill pattern; keeps the loads live
+    if (acc.x == 0x9E3779B9u && acc.y == 0x7F4A7C15u) sink[0] = acc.z ^ acc.w;
+}
+
+__global__ __launch_bounds__(256) void probe_write_kernel(u32x4* __restrict__ b, size_t n) {
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += stride) {
+        const u32x4 v = {(uint32_t)i, (uint32_t)(i >> 32), 0x5EEDu, 1u};
+        __builtin_nontemporal_store(v, b + i);
+    }
+}
+
+__global__ __launch_bounds__(256) void probe_copy_kernel(const u32x4* __restrict__ a, u32x4* __restrict__ b,
+                                                         size_t n) {
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    for (; i + 3 * stride < n; i += 4 * stride) {
+        const u32x4 x0 = a[i], x1 = a[i + stride], x2 = a[i + 2 * stride], x3 = a[i + 3 * stride];
+        __builtin_nontemporal_store(x0, b + i);
+        __builtin_nontemporal_store(x1, b + i + stride);
+        __builtin_nontemporal_store(x2, b + i + 2 * stride);
+        __builtin_nontemporal_store(x3, b + i + 3 * stride);
+    }
+    for (; i < n; i += stride) __builtin_nontemporal_store(a[i], b + i);
+}
+
+// kind 0 read a, 1 write b, 2 copy a -> b; n16 = 16-byte words.
+hipError_t launch_probe(int kind, const void* a, void* b, size_t n16, uint32_t n_cu, hipStream_t stream) {
+    const uint32_t grid = n_cu * 16u;
+    if (kind == 0)
+        hipLaunchKernelGGL(probe_read_kernel, dim3(grid), dim3(256), 0, stream, (const u32x4*)a, n16, (uint32_t*)b);
+    else if (kind == 1)
+        hipLaunchKernelGGL(probe_write_kernel, dim3(grid), dim3(256), 0, stream, (u32x4*)b, n16);
+    else
+        hipLaunchKernelGGL(probe_copy_kernel, dim3(grid), dim3(256), 0, stream, (const u32x4*)a, (u32x4*)b, n16);
+    return hipGetLastError();
+}
+
+}  // namespace crdt

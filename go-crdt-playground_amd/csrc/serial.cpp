@@ -199,6 +199,7 @@ int crdt_batch_dump(const crdt_awset_batch* b, void* buf, size_t cap, size_t* le
     if (!b || !b->offsets || (b->n_docs && !b->vv) || !len) return CRDT_E_INVALID;
     uint64_t n = 0;
     for (uint32_t d = 0; d < b->n_docs; ++d) n += live_of(b, d);
+    if (n >= (1ull << 32)) return CRDT_E_CAPACITY;  // per-doc offsets are u32 in the image
     const size_t need = kHeader + offs_bytes(b->n_docs) + ents_bytes(n) + 8 * (size_t)b->n_docs * b->R + 8;
     *len = need;
     if (!buf) return CRDT_OK;
@@ -241,7 +242,7 @@ int crdt_batch_info(const void* buf, size_t len, uint32_t* n_docs, uint32_t* R, 
     memcpy(&r, p + 12, 4);
     memcpy(&n, p + 16, 8);
     if (r == 0 || r > CRDT_MAX_R) return CRDT_E_INVALID;
-    if (n > (1ull << 40) || nd > (1u << 31)) return CRDT_E_INVALID;
+    if (n >= (1ull << 32) || nd > (1u << 31)) return CRDT_E_INVALID;  // matches crdt_batch_dump
     const size_t need = kHeader + offs_bytes(nd) + ents_bytes(n) + 8 * (size_t)nd * r + 8;
     if (len != need) return CRDT_E_INVALID;
     uint64_t h;

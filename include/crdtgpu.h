@@ -205,6 +205,18 @@ int crdt_gen_zipf_async(crdt_ctx* ctx, uint64_t seed, uint32_t n_docs, const uin
 int crdt_gen_replicas_async(crdt_ctx* ctx, uint64_t seed, uint32_t n_docs, uint32_t replicas, uint32_t entries,
                             const crdt_awset_out* dst, const crdt_src_batch* srcs, void* stream);
 
+/* ---- box bandwidth probes (not a merge; bench.py's roofline context) ------
+ * Times `reps` launches of a streaming kernel over caller-owned device memory
+ * on the context's stream (after one untimed launch) and returns the HBM rate
+ * in GB/s (1e9 B/s): READ reads `bytes` of a (16 B per lane, four loads in
+ * flight), WRITE writes `bytes` to b (16 B non-temporal stores), COPY reads a
+ * and writes b (counts 2 x bytes).  READ needs b as a 4-byte sink.  Use
+ * buffers well above the 256 MiB Infinity Cache.  Synchronous. */
+#define CRDT_PROBE_READ 0
+#define CRDT_PROBE_WRITE 1
+#define CRDT_PROBE_COPY 2
+int crdt_bw_probe(crdt_ctx* ctx, int kind, const void* a, void* b, size_t bytes, int reps, double* gbs);
+
 /* ---- batched local operations: the state producers -----
  * Each document receives an ordered op list, applied to its replica state
  * (AWSet entries + VV, and for AWSetDelta its Deleted tombstones) as the
@@ -344,6 +356,9 @@ int crdt_awset_fold_batch(crdt_ctx* ctx, int mode, const crdt_awset_batch* dst, 
 /* ---- host-side validation of a packed batch (no GPU) -------------------- */
 int crdt_validate_batch(const crdt_awset_batch* b);
 int crdt_validate_src_batch(const crdt_src_batch* s);
+/* tombstones of n_docs documents: monotone offsets, counts <= slots, keys
+ * strictly ascending per document (crdt_awset_apply_batch runs it first). */
+int crdt_validate_tomb_batch(const crdt_tomb_batch* t, uint32_t n_docs);
 
 #ifdef __cplusplus
 }

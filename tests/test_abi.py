@@ -59,6 +59,26 @@ def test_validate_src_batch():
     assert crdtgpu.validate_src(badt) == crdtgpu.CRDT_E_UNSORTED
 
 
+def test_validate_tomb_batch():
+    from crdtgpu.batch import TombBatch
+    from crdtgpu.engine import validate_tombs
+
+    u32, u64 = np.uint32, np.uint64
+
+    def tb(offs, keys, counts=None):
+        n = len(keys)
+        return TombBatch(np.array(offs, u32), np.array(keys, u64), np.zeros(n, u32), np.ones(n, u64),
+                         None if counts is None else np.array(counts, u32))
+
+    assert validate_tombs(tb([0, 2, 3], [1, 5, 2]), 2) == 0
+    assert validate_tombs(tb([0, 2, 3], [5, 1, 2]), 2) == crdtgpu.CRDT_E_UNSORTED
+    assert validate_tombs(tb([0, 2, 3], [1, 1, 2]), 2) == crdtgpu.CRDT_E_UNSORTED
+    assert validate_tombs(tb([0, 2, 3], [1, 5, 2], counts=[3, 1]), 2) == crdtgpu.CRDT_E_CAPACITY
+    assert validate_tombs(tb([0, 3, 2], [1, 2, 5]), 2) == crdtgpu.CRDT_E_INVALID
+    # counts below capacity: the unsorted tail past the live count is not read
+    assert validate_tombs(tb([0, 3, 3], [1, 5, 0], counts=[2, 0]), 2) == 0
+
+
 def test_product_has_no_cpu_fallback():
     """The product package must not import the oracle or ship a CPU merge."""
     import os

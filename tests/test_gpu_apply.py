@@ -84,6 +84,20 @@ def test_apply_errors(eng):
     # engine is usable after errors
     op = OpBatch.from_lists([[(crdtgpu.CRDT_OP_DEL, 1)], ddk[:1]], [R + 3, 1])
     check_same(eng, st, op, None, R, 2)
+    # malformed tombstone batches are refused on the host before any launch
+    # (the kernel sizes its staging by the counts and binary-searches the keys)
+    u32, u64 = np.uint32, np.uint64
+    ops = OpBatch.from_lists([[(add, 3)], [(add, 4)]], [0, 1])
+    over = TombBatch(np.array([0, 1, 2], u32), np.array([2, 7], u64), np.zeros(2, u32), np.ones(2, u64),
+                     counts=np.array([2, 1], u32))
+    with pytest.raises(crdtgpu.CrdtError) as ei:
+        eng.apply(st, ops, over)
+    assert ei.value.code == crdtgpu.CRDT_E_CAPACITY
+    unsorted = TombBatch(np.array([0, 2, 2], u32), np.array([7, 2], u64), np.zeros(2, u32), np.ones(2, u64))
+    with pytest.raises(crdtgpu.CrdtError) as ei:
+        eng.apply(st, ops, unsorted)
+    assert ei.value.code == crdtgpu.CRDT_E_UNSORTED
+    check_same(eng, st, ops, None, R, 2)  # still usable
 
 
 def test_apply_device_async(eng, torch):
