@@ -57,14 +57,19 @@ def _worker(rank, world, port, q):
         eng.gen_replicas_async(seed, N_DOCS, P, E, D, S)
         out = OutBuffers(N_DOCS, R, N_DOCS * E * P, device=dev)
         eng.fold_async(CRDT_FOLD_AWSET, D.as_batch(), S, out)
-        summ = torch.zeros(R, dtype=torch.int64, device=dev)
-        eng.causal_context_async(out.vv, N_DOCS, R, summ)
         eng.sync()
         # this rank's fold, every document, vs the oracle
         torch.cuda.synchronize()
         rc, want = oracle.fold(CRDT_FOLD_AWSET, host_out(D, torch).as_batch(), S.numpy())
         assert rc == 0
         assert_same_all(host_out(out, torch), want, N_DOCS, R)
+        # the generated clocks saturate over thousands of docs (every rank's max
+        # is 31); one rank-specific clock word per rank makes the summaries differ
+        out.vv[3 * R + rank] = 1000 + rank
+        want.vv[3 * R + rank] = 1000 + rank
+        summ = torch.zeros(R, dtype=torch.int64, device=dev)
+        eng.causal_context_async(out.vv, N_DOCS, R, summ)
+        eng.sync()
         local = summ.cpu().numpy().view(np.uint64).tolist()
         oracle_local = oracle.causal_context(want.vv, N_DOCS, R).tolist()
         glob = cdist.u64_max_allreduce(dist, summ.cpu()).numpy().view(np.uint64).tolist()
