@@ -16,15 +16,23 @@ the join/fold kernels through ``crdt_awset_join_batch`` /
 local ops (Add, Del, Clone, ...) are per-replica host state changes, as in the
 reference; they are not part of the batched hot path.
 
-Differences from the Go code, all at inputs where Go panics or is ambiguous:
-  * a batch's version vectors are zero-padded to the longest one (R <= 64).
-    The kernels flag HasDot at actor == R; for a shorter vector the panic at
-    actor == len(vv) is found on the host before the launch -- exactly for
-    MergeBatch (the HasDot calls of awset.go:133 and :152 are replayed on the
-    keys alone).  Folds over vectors of unequal lengths read the pad instead
-    of panicking; equal-length vectors (every reference test) are exact.
-  * where Go panics (actor == len(vv)), the merge raises CrdtError
-    (CRDT_E_ACTOR_RANGE) and leaves the destination untouched.
+Version vectors of unequal lengths:
+  * a batch's version vectors are zero-padded to one width R (<= 64).  When
+    every vector of a document has length R, the kernels flag HasDot/Counter
+    at actor == R exactly where Go panics (crdt-misc.go:29,37).
+  * a document with a shorter vector is replayed on the host before the
+    launch (_replay_checks): every HasDot and Counter call of the reference,
+    in order, on the unpadded vectors -- Counter(src.Actor)
+    (awset-delta_test.go:53), MakeDeltaMergeData's HasDot (:85), phase 1
+    (awset.go:133, awset-delta_test.go:137), phase 2 (awset.go:152,
+    awset-delta_test.go:153).  A panic there raises CrdtError
+    (CRDT_E_ACTOR_RANGE), nothing applied; the merged entries still come from
+    the GPU.  R is chosen so that no actor of such a document equals R (the
+    kernels' flag would otherwise fire where Go returns false).
+  * the one input the padded layout cannot express: a dot with counter 0 at
+    an actor between len(vv) and R, where Go's HasDot says false and the pad
+    says true.  Counter-0 dots are unreachable (Add bumps first, awset.go:92),
+    so such a batch is refused with CRDT_E_INVALID.
 """
 
 from __future__ import annotations
@@ -205,14 +213,113 @@ def _unpack(dsts, out, names, R, widths):
         dst.VersionVector = VersionVector(out.vv[d * R:d * R + widths[d]].tolist())
 
 
+class _GoPanic(Exception):
+    pass
+
+
+class _Check:
+    """HasDot / Counter as Go evaluates them on the unpadded vectors
+    (crdt-misc.go:28-41), noting where the zero-padded width R answers
+    differently (a counter-0 dot at len(vv) < actor < R)."""
+
+    def __init__(self, R):
+        self.R, self.pad_differs = R, False
+
+    def has(self, vv, d: Dot) -> bool:
+        n = len(vv)
+        if n < d.Actor:
+            if d.Actor < self.R and d.Counter == 0:
+                self.pad_differs = True
+            return False
+        if d.Actor == n:
+            raise _GoPanic
+        return vv[d.Actor] >= d.Counter
+
+    @staticmethod
+    def counter(vv, a: int) -> int:
+        n = len(vv)
+        if n < a:
+            return 0
+        if a == n:
+            raise _GoPanic
+        return vv[a]
+
+
+def _replay_checks(mode, dst, srcs, R) -> Optional[str]:
+    """Replay dst.Merge(src) for src in srcs, in order, on maps with the
+    reference's rules -- (*AWSet).merge awset.go:107-161, (*AWSetDelta).Merge
+    awset-delta_test.go:51-65, MakeDeltaMergeData :79-105, deltaMerge :107-166
+    -- only to find whether Go panics ("panic") or the padded layout would
+    differ ("pad"); None otherwise.  Whether Go panics does not depend on its
+    random map order: every call site runs unless an earlier one panicked."""
+    ck = _Check(R)
+    V = list(dst.VersionVector)
+    E = dict(dst.Entries)
+    try:
+        for s in srcs:
+            full = mode != abi.CRDT_FOLD_DELTA or ck.counter(V, s.Actor) <= 0
+            if full:
+                changed, dele = s.Entries, {}
+            else:
+                changed = {k: d for k, d in s.Entries.items() if not ck.has(V, d)}
+                dele = {}
+                for k, x in (getattr(s, "Deleted", None) or {}).items():
+                    m = s.Entries.get(k)
+                    if m is None or not (m.Actor != x.Actor or m.Counter > x.Counter):
+                        dele[k] = x
+                if not changed and not dele:
+                    continue  # awset-delta_test.go:60: no deltaMerge, no VersionVector.Merge
+            for k, sd in changed.items():
+                if k in E or not ck.has(V, sd):
+                    E[k] = sd
+            if full:
+                for k in [k for k in E if k not in s.Entries]:
+                    if ck.has(s.VersionVector, E[k]):
+                        del E[k]
+            else:
+                for k, x in dele.items():
+                    if k in E and not ck.has(V, x):
+                        del E[k]
+            sv = list(s.VersionVector)
+            V = [max(x, y) for x, y in zip(V, sv)] + V[len(sv):] + sv[len(V):]
+    except _GoPanic:
+        return "panic"
+    return "pad" if ck.pad_differs else None
+
+
+def _doc_actors(mode, states):
+    a = set()
+    for i, s in enumerate(states):
+        a.update(d.Actor for d in s.Entries.values())
+        a.update(d.Actor for d in (getattr(s, "Deleted", None) or {}).values())
+        if i and mode == abi.CRDT_FOLD_DELTA:
+            a.add(s.Actor)
+    return a
+
+
+def _ragged_checks(mode, docs, what) -> int:
+    """The padded width R of a batch (docs[i] = [dst, src...]) and the host
+    checks of its documents with a vector shorter than R (module docstring)."""
+    R = _width([s for doc in docs for s in doc])
+    short = lambda doc, w: any(len(s.VersionVector) < w for s in doc)  # noqa: E731
+    for w in range(R, abi.CRDT_MAX_R + 1):
+        if not any(short(doc, w) and w in _doc_actors(mode, doc) for doc in docs):
+            break
+    else:
+        raise abi.CrdtError(abi.CRDT_E_INVALID, "%s: every padded width collides with an actor" % what)
+    for doc in docs:
+        if short(doc, w):
+            r = _replay_checks(mode, doc[0], doc[1:], w)
+            if r == "panic":
+                raise abi.CrdtError(abi.CRDT_E_ACTOR_RANGE, "%s: HasDot/Counter at actor == len(vv)" % what)
+            if r == "pad":
+                raise abi.CrdtError(abi.CRDT_E_INVALID, "%s: counter-0 dot beyond a shorter version vector" % what)
+    return w
+
+
 def _join_panics(dst: "AWSet", src: "AWSet") -> bool:
-    """Would dst.Merge(src) panic in Go at a HasDot with actor == len(vv)?  The
-    reference evaluates dstVV.HasDot(s) for every src-only key (awset.go:133)
-    and srcVV.HasDot(d) for every dst-only key (:152)."""
-    ld, ls = len(dst.VersionVector), len(src.VersionVector)
-    if any(k not in dst.Entries and s.Actor == ld for k, s in src.Entries.items()):
-        return True
-    return any(k not in src.Entries and d.Actor == ls for k, d in dst.Entries.items())
+    """Would dst.Merge(src) panic in Go at a HasDot with actor == len(vv)?"""
+    return _replay_checks(abi.CRDT_FOLD_AWSET, dst, [src], abi.CRDT_MAX_R + 1) == "panic"
 
 
 def MergeBatch(dsts: Sequence[AWSet], srcs: Sequence[AWSet], engine: Optional[Engine] = None) -> None:
@@ -222,10 +329,7 @@ def MergeBatch(dsts: Sequence[AWSet], srcs: Sequence[AWSet], engine: Optional[En
     if not dsts:
         return
     states = list(dsts) + list(srcs)
-    R = _width(states)
-    for a, b in zip(dsts, srcs):  # vectors shorter than R: their panic point is below the kernels' actor == R
-        if (len(a.VersionVector) < R or len(b.VersionVector) < R) and _join_panics(a, b):
-            raise abi.CrdtError(abi.CRDT_E_ACTOR_RANGE, "MergeBatch: HasDot at actor == len(vv)")
+    R = _ragged_checks(abi.CRDT_FOLD_AWSET, [[a, b] for a, b in zip(dsts, srcs)], "MergeBatch")
     ids = _intern(states)
     names = {i: k for k, i in ids.items()}
     db = AWSetBatch.from_docs(R, [(_entries(s.Entries, ids), _pad(s.VersionVector, R)) for s in dsts])
@@ -241,9 +345,10 @@ def _fold(mode, dsts, srcs_per_dst, engine):
     if not dsts:
         return
     states = list(dsts) + [s for lst in srcs_per_dst for s in lst]
+    R = _ragged_checks(mode, [[d] + list(lst) for d, lst in zip(dsts, srcs_per_dst)],
+                       "DeltaMergeBatch" if mode == abi.CRDT_FOLD_DELTA else "FoldBatch")
     ids = _intern(states)
     names = {i: k for k, i in ids.items()}
-    R = _width(states)
     db = AWSetBatch.from_docs(R, [(_entries(s.Entries, ids), _pad(s.VersionVector, R)) for s in dsts])
     per_doc = [[(s.Actor, _pad(s.VersionVector, R), _entries(s.Entries, ids),
                  _entries(getattr(s, "Deleted", None), ids)) for s in lst] for lst in srcs_per_dst]

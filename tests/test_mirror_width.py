@@ -76,3 +76,67 @@ def test_join_panic_check_matches_reference_for_unequal_lengths():
         assert _join_panics(a, b) == want
         panics += want
     assert panics > 200
+
+
+def _ragged_chain(rng, delta, n_src):
+    """dst + ordered sources with VVs of 1..4 words and actors up to 4, so that
+    actor == len(vv) of a shorter vector is frequent."""
+    def st(tombs):
+        e, vv, dele = _rand(rng, rng.randint(1, 4), 8, tombs)
+        e = [(k, rng.randrange(5), c) for k, _, c in e]
+        dele = [(k, rng.randrange(5), c) for k, _, c in dele]
+        return e, vv, dele
+    dst = st(False)
+    return dst, [(rng.randrange(5),) + st(delta) for _ in range(n_src)]
+
+
+def test_fold_replay_checks_match_reference_panics():
+    """_replay_checks (the mirrors' host check for folds over VVs of unequal
+    lengths) says "panic" exactly where the map restatement of the reference
+    raises GoPanic: Counter(src.Actor) awset-delta_test.go:53, the HasDot of
+    MakeDeltaMergeData :85, phase 1 awset.go:133 / :137, phase 2 awset.go:152 /
+    tombstones :153 -- for AWSet folds and AWSetDelta folds."""
+    from crdtgpu.awset import _replay_checks
+
+    rng = random.Random(73)
+    seen = {True: 0, False: 0}
+    for delta in (False, True):
+        mode = abi.CRDT_FOLD_DELTA if delta else abi.CRDT_FOLD_AWSET
+        cls = ref.AWSetDelta if delta else ref.AWSet
+        for _ in range(3000):
+            (e0, v0, _), chain = _ragged_chain(rng, delta, rng.randint(1, 4))
+            x = ref_state(e0, v0, cls=cls)
+            try:
+                for act, e, svv, dele in chain:
+                    x.Merge(ref_state(e, svv, actor=act, cls=cls, deleted=dele if delta else None))
+                want = False
+            except ref.GoPanic:
+                want = True
+            got = _replay_checks(mode, _mirror(0, e0, v0, []),
+                                 [_mirror(act, e, svv, dele if delta else []) for act, e, svv, dele in chain], 5)
+            assert (got == "panic") == want, (delta, e0, v0, chain)
+            seen[want] += 1
+    assert seen[True] > 500 and seen[False] > 500
+
+
+def test_ragged_width_avoids_actor_collisions():
+    """The padded width R skips values some actor of a short document takes
+    (the kernels flag actor == R where Go, on the shorter vector, says false)."""
+    from crdtgpu.awset import AWSet, _ragged_checks
+
+    a = AWSet(0, [1, 1], {"x": Dot(2, 1)})     # shorter than the longest vector: a "short" document
+    b = AWSet(1, [1, 1, 1], {"x": Dot(3, 1)})  # actor 3 == the longest length: R = 3 collides, R = 4 does not
+    assert _ragged_checks(abi.CRDT_FOLD_AWSET, [[a, b]], "t") == 4
+    c = AWSet(0, [1, 1, 1], {"y": Dot(3, 1)})
+    d = AWSet(1, [1, 1, 1], {"y": Dot(0, 1)})
+    assert _ragged_checks(abi.CRDT_FOLD_AWSET, [[c, d]], "t") == 3  # equal lengths: the kernels are exact at R
+
+    # a counter-0 src dot past the end of the shorter dst vector: Go's HasDot says
+    # false (add), the zero pad would say true (skip) -> refused, CRDT_E_INVALID
+    import pytest
+
+    e = AWSet(0, [1], {})
+    f = AWSet(1, [1, 1, 1], {"q": Dot(2, 0)})
+    with pytest.raises(abi.CrdtError) as ei:
+        _ragged_checks(abi.CRDT_FOLD_AWSET, [[e, f]], "t")
+    assert ei.value.code == abi.CRDT_E_INVALID

@@ -229,3 +229,68 @@ def test_apply_batch_matches_reference_calls():
     with pytest.raises(CrdtError):
         ApplyBatch([a, b], [[("Add", "x")], [("Add", "y")]])
     assert a.Entries == {} and list(a.VersionVector) == [0, 0]
+
+
+@pytest.mark.parametrize("kind", ["join", "fold", "delta"])
+def test_ragged_version_vectors_match_reference(kind):
+    """Version vectors of unequal lengths in one batch (padded to one width on
+    the device): every document ends exactly as the map restatement of the
+    reference leaves it (entries, dots, clock and its length), and a document
+    whose merge panics in Go (HasDot / Counter at actor == len(vv) of the
+    unpadded vector) raises CRDT_E_ACTOR_RANGE with its destination untouched."""
+    import random
+
+    from crdtgpu import CrdtError, abi
+    from helpers import ref_state
+    from oracle import awset_ref as ref
+    from test_mirror_width import _ragged_chain
+
+    rng = random.Random({"join": 81, "fold": 82, "delta": 83}[kind])
+    delta = kind == "delta"
+    cls, rcls = (AWSetDelta, ref.AWSetDelta) if delta else (AWSet, ref.AWSet)
+
+    def mirror(actor, e, vv, dele):
+        m = cls(actor, vv, {"%012d" % k: Dot(a, c) for k, a, c in e})
+        if delta and dele:
+            m.Deleted = {"%012d" % k: Dot(a, c) for k, a, c in dele}
+        return m
+
+    ok, panics = [], []
+    for _ in range(600):
+        (e0, v0, _), chain = _ragged_chain(rng, delta, 1 if kind == "join" else rng.randint(1, 4))
+        x = ref_state(e0, v0, cls=rcls)
+        try:
+            for act, e, svv, dele in chain:
+                x.Merge(ref_state(e, svv, actor=act, cls=rcls, deleted=dele if delta else None))
+            ok.append((e0, v0, chain, x))
+        except ref.GoPanic:
+            panics.append((e0, v0, chain))
+    assert len(ok) > 100 and len(panics) > 50
+
+    def run(dsts, chains):
+        srcs = [[mirror(a, e, v, d) for a, e, v, d in ch] for ch in chains]
+        if kind == "join":
+            MergeBatch(dsts, [s[0] for s in srcs])
+        elif kind == "fold":
+            FoldBatch(dsts, srcs)
+        else:
+            DeltaMergeBatch(dsts, srcs)
+
+    dsts = [mirror(0, e0, v0, []) for e0, v0, _, _ in ok]
+    run(dsts, [ch for _, _, ch, _ in ok])
+    for m, (_, _, _, x) in zip(dsts, ok):
+        assert {k: (d.Actor, d.Counter) for k, d in m.Entries.items()} == \
+            {k: (d.actor, d.counter) for k, d in x.Entries.items()}
+        assert list(m.VersionVector) == list(x.VersionVector)
+    for e0, v0, chain in panics[:40]:
+        d = mirror(0, e0, v0, [])
+        with pytest.raises(CrdtError) as ei:
+            run([d], [chain])
+        assert ei.value.code == abi.CRDT_E_ACTOR_RANGE
+        assert list(d.VersionVector) == v0 and len(d.Entries) == len(e0)
+    # the one input the padded layout cannot express: a counter-0 dot between a
+    # shorter vector's end and the batch width (Go: HasDot false; pad: true)
+    a, b = AWSet(0, [1], {}), AWSet(1, [1, 1, 1], {"q": Dot(2, 0)})
+    with pytest.raises(CrdtError) as ei:
+        MergeBatch([a], [b])
+    assert ei.value.code == abi.CRDT_E_INVALID

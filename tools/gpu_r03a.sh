@@ -6,7 +6,7 @@ set -u
 cd "$(dirname "$0")/.."
 source tools/gpu_step.sh
 TAILN=4
-step new_tests 300 python -u -m pytest tests/test_gpu_probe.py tests/test_gpu_multirank.py tests/test_gpu_apply.py -x -v --timeout 250 --timeout-method thread
+step new_tests 300 python -u -m pytest tests/test_gpu_probe.py tests/test_gpu_multirank.py tests/test_gpu_apply.py tests/test_scenarios_gpu.py -x -v --timeout 250 --timeout-method thread
 grep -q " failed\| error" gpurun_out/new_tests.log && exit 1
 step gpu_tests 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread
 grep -q " failed\| error" gpurun_out/gpu_tests.log && exit 1
