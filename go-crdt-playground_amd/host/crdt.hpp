@@ -15,9 +15,13 @@
 // Where the Go code panics (HasDot/Counter at actor == len(vv), Add with the
 // actor outside the vector), this API throws crdt::Error carrying the C ABI
 // code (CRDT_E_ACTOR_RANGE); a failed merge leaves its destinations untouched.
-// Version vectors of one batch are zero-padded to the longest (<= 64); for a
-// join the panic at actor == len(vv) of a shorter vector is found on the host
-// (detail::join_panics), folds over unequal lengths read the pad.
+// Version vectors of one batch are zero-padded to one width R (<= 64).  A
+// document with a vector shorter than R is replayed on the host before the
+// launch (detail::replay_checks: every HasDot / Counter call of the reference
+// on the unpadded vectors), so Go's panic at actor == len(vv) is found exactly;
+// R is chosen clear of such documents' actors (the kernels flag actor == R).
+// A counter-0 dot between a shorter vector's end and R (unreachable: Add bumps
+// first) is refused with CRDT_E_INVALID: the zero pad cannot express it.
 #pragma once
 
 #include <algorithm>
@@ -329,17 +333,128 @@ void intern_all(Batch& b, size_t n, F&& states_of) {
 }  // namespace detail
 
 namespace detail {
-// Would dst.Merge(src) panic in Go at a HasDot with actor == len(vv)?  The
-// reference evaluates dstVV.HasDot(s) for every src-only key (awset.go:133)
-// and srcVV.HasDot(d) for every dst-only key (:152).  The kernels flag actor ==
-// R; this covers vectors shorter than the batch's R.
-inline bool join_panics(const AWSet& dst, const AWSet& src) {
-    const size_t ld = dst.versionVector.size(), ls = src.versionVector.size();
-    for (auto& kv : src.entries)
-        if (kv.second.actor == ld && !dst.entries.count(kv.first)) return true;
-    for (auto& kv : dst.entries)
-        if (kv.second.actor == ls && !src.entries.count(kv.first)) return true;
-    return false;
+struct GoPanic {};
+
+// HasDot / Counter as Go evaluates them on the unpadded vectors
+// (crdt-misc.go:28-41), noting where the zero-padded width R answers
+// differently (a counter-0 dot at len(vv) < actor < R).
+struct Checks {
+    size_t R;
+    bool pad_differs = false;
+    bool has(const std::vector<uint64_t>& vv, const Dot& d) {
+        const size_t n = vv.size();
+        if (n < d.actor) {
+            if (d.actor < R && d.counter == 0) pad_differs = true;
+            return false;
+        }
+        if (d.actor == n) throw GoPanic{};
+        return vv[d.actor] >= d.counter;
+    }
+    static uint64_t counter(const std::vector<uint64_t>& vv, Actor a) {
+        if (vv.size() < a) return 0;
+        if (a == vv.size()) throw GoPanic{};
+        return vv[a];
+    }
+};
+
+enum { kReplayOk = 0, kReplayPanic = 1, kReplayPad = 2 };
+
+// Replay dst.Merge(src) for src in srcs, in order, on maps with the
+// reference's rules -- (*AWSet).merge awset.go:107-161, (*AWSetDelta).Merge
+// awset-delta_test.go:51-65, MakeDeltaMergeData :79-105, deltaMerge :107-166
+// -- only to find whether Go panics or the padded layout would differ.
+// Whether Go panics does not depend on its random map order.
+inline int replay_checks(int mode, const AWSet& dst, const std::vector<const AWSet*>& srcs, size_t R) {
+    Checks ck{R};
+    std::vector<uint64_t> V(dst.versionVector.begin(), dst.versionVector.end());
+    Entries E = dst.entries;
+    try {
+        for (const AWSet* s : srcs) {
+            const bool full = mode != CRDT_FOLD_DELTA || Checks::counter(V, s->actor) == 0;
+            Entries changed, dele;
+            if (!full) {
+                for (auto& kv : s->entries)
+                    if (!ck.has(V, kv.second)) changed.emplace(kv.first, kv.second);
+                if (auto* del = s->deleted_map())
+                    for (auto& kv : *del) {
+                        auto it = s->entries.find(kv.first);
+                        if (it == s->entries.end() ||
+                            !(it->second.actor != kv.second.actor || it->second.counter > kv.second.counter))
+                            dele.emplace(kv.first, kv.second);
+                    }
+                if (changed.empty() && dele.empty()) continue;  // awset-delta_test.go:60: nothing, not even the VV
+            }
+            for (auto& kv : full ? s->entries : changed)
+                if (E.count(kv.first) || !ck.has(V, kv.second)) E[kv.first] = kv.second;
+            if (full) {
+                for (auto it = E.begin(); it != E.end();) {
+                    if (!s->entries.count(it->first) && ck.has(s->versionVector, it->second))
+                        it = E.erase(it);
+                    else
+                        ++it;
+                }
+            } else {
+                for (auto& kv : dele) {
+                    auto it = E.find(kv.first);
+                    if (it != E.end() && !ck.has(V, kv.second)) E.erase(it);
+                }
+            }
+            const auto& sv = s->versionVector;
+            for (size_t i = 0; i < sv.size(); ++i) {
+                if (i < V.size())
+                    V[i] = std::max<uint64_t>(V[i], sv[i]);
+                else
+                    V.push_back(sv[i]);
+            }
+        }
+    } catch (const GoPanic&) {
+        return kReplayPanic;
+    }
+    return ck.pad_differs ? kReplayPad : kReplayOk;
+}
+
+// The padded width R of a batch whose document d holds states_of(d) (dst
+// first), after the host checks of its documents with a vector shorter than R.
+template <typename F>
+size_t ragged_checks(int mode, size_t n_docs, F&& states_of, const char* what) {
+    size_t R = 1;
+    for (size_t d = 0; d < n_docs; ++d)
+        for (const AWSet* s : states_of(d)) R = std::max(R, s->versionVector.size());
+    if (R > CRDT_MAX_R) throw Error(CRDT_E_INVALID, "version vector longer than CRDT_MAX_R");
+    auto is_short = [](const std::vector<const AWSet*>& doc, size_t w) {
+        for (const AWSet* s : doc)
+            if (s->versionVector.size() < w) return true;
+        return false;
+    };
+    auto has_actor = [mode](const std::vector<const AWSet*>& doc, size_t w) {
+        for (size_t i = 0; i < doc.size(); ++i) {
+            if (i && mode == CRDT_FOLD_DELTA && doc[i]->actor == w) return true;
+            for (auto& kv : doc[i]->entries)
+                if (kv.second.actor == w) return true;
+            if (auto* del = doc[i]->deleted_map())
+                for (auto& kv : *del)
+                    if (kv.second.actor == w) return true;
+        }
+        return false;
+    };
+    size_t w = R;
+    for (;; ++w) {
+        if (w > CRDT_MAX_R) throw Error(CRDT_E_INVALID, std::string(what) + ": every padded width collides with an actor");
+        bool clash = false;
+        for (size_t d = 0; d < n_docs && !clash; ++d) {
+            const auto doc = states_of(d);
+            clash = is_short(doc, w) && has_actor(doc, w);
+        }
+        if (!clash) break;
+    }
+    for (size_t d = 0; d < n_docs; ++d) {
+        const auto doc = states_of(d);
+        if (!is_short(doc, w)) continue;
+        const int r = replay_checks(mode, *doc[0], std::vector<const AWSet*>(doc.begin() + 1, doc.end()), w);
+        if (r == kReplayPanic) throw Error(CRDT_E_ACTOR_RANGE, std::string(what) + ": HasDot/Counter at actor == len(vv)");
+        if (r == kReplayPad) throw Error(CRDT_E_INVALID, std::string(what) + ": counter-0 dot beyond a shorter version vector");
+    }
+    return w;
 }
 }  // namespace detail
 
@@ -349,13 +464,9 @@ inline void MergeBatch(const std::vector<AWSet*>& dsts, const std::vector<const 
     if (dsts.size() != srcs.size()) throw Error(CRDT_E_INVALID, "MergeBatch: length mismatch");
     if (dsts.empty()) return;
     detail::Batch b;
-    for (size_t i = 0; i < dsts.size(); ++i)
-        b.R = std::max({b.R, dsts[i]->versionVector.size(), srcs[i]->versionVector.size()});
-    if (b.R > CRDT_MAX_R) throw Error(CRDT_E_INVALID, "version vector longer than CRDT_MAX_R");
-    for (size_t i = 0; i < dsts.size(); ++i)
-        if ((dsts[i]->versionVector.size() < b.R || srcs[i]->versionVector.size() < b.R) &&
-            detail::join_panics(*dsts[i], *srcs[i]))
-            throw Error(CRDT_E_ACTOR_RANGE, "MergeBatch: HasDot at actor == len(vv)");
+    b.R = detail::ragged_checks(
+        CRDT_FOLD_AWSET, dsts.size(), [&](size_t d) { return std::vector<const AWSet*>{dsts[d], srcs[d]}; },
+        "MergeBatch");
     detail::intern_all(b, dsts.size(), [&](size_t d) { return std::vector<const AWSet*>{dsts[d], srcs[d]}; });
     std::vector<AWSet*> sv;
     for (auto* s : srcs) sv.push_back(const_cast<AWSet*>(s));
@@ -413,11 +524,14 @@ inline void fold(int mode, const std::vector<AWSet*>& dsts, const std::vector<st
     if (dsts.size() != srcs.size()) throw Error(CRDT_E_INVALID, "fold: length mismatch");
     if (dsts.empty()) return;
     Batch b;
-    for (size_t i = 0; i < dsts.size(); ++i) {
-        b.R = std::max(b.R, dsts[i]->versionVector.size());
-        for (auto* s : srcs[i]) b.R = std::max(b.R, s->versionVector.size());
-    }
-    if (b.R > CRDT_MAX_R) throw Error(CRDT_E_INVALID, "version vector longer than CRDT_MAX_R");
+    b.R = ragged_checks(
+        mode, dsts.size(),
+        [&](size_t d) {
+            std::vector<const AWSet*> v{dsts[d]};
+            v.insert(v.end(), srcs[d].begin(), srcs[d].end());
+            return v;
+        },
+        mode == CRDT_FOLD_DELTA ? "DeltaMergeBatch" : "FoldBatch");
     intern_all(b, dsts.size(), [&](size_t d) {
         std::vector<const AWSet*> v{dsts[d]};
         v.insert(v.end(), srcs[d].begin(), srcs[d].end());

@@ -176,6 +176,40 @@ static void TestPanicsBecomeErrors() {
     CHECK(a.entries.size() == 1);  // untouched
 }
 
+// Version vectors of unequal lengths (zero-padded on the device): Go's panics
+// at actor == len(vv) of the shorter vector, found by the host replay, and an
+// exact result where Go does not panic.
+static void TestRaggedVectors() {
+    auto throws_range = [](auto&& fn) {
+        try {
+            fn();
+        } catch (const Error& e) {
+            return e.code == CRDT_E_ACTOR_RANGE;
+        }
+        return false;
+    };
+    {  // Counter(src.Actor) with src.Actor == len(dst VV)   awset-delta_test.go:53
+        AWSetDelta d(0, {5, 5}), s(2, {1, 1, 1});
+        CHECK(throws_range([&] { d.Merge(s); }));
+        CHECK(d.versionVector == (VersionVector{5, 5}));
+    }
+    {  // tombstone HasDot on the shorter dst VV             awset-delta_test.go:153
+        AWSetDelta d(0, {3, 3}), s(1, {1, 2, 1});
+        d.entries["k"] = Dot{0, 1};
+        s.deleted["k"] = Dot{2, 1};
+        CHECK(throws_range([&] { d.Merge(s); }));
+        CHECK(d.entries.size() == 1);
+    }
+    {  // no panic: a src-only key whose actor lies past the shorter dst VV is added
+        AWSet d(0, {2}), s(2, {0, 0, 1});
+        d.entries["a"] = Dot{0, 1};
+        d.entries["b"] = Dot{0, 2};
+        s.entries["c"] = Dot{2, 1};
+        FoldBatch({&d}, {{&s}});
+        expect(d, {{"a", {0, 1}}, {"b", {0, 2}}, {"c", {2, 1}}}, {2, 0, 1});
+    }
+}
+
 static void TestBatches() {
     std::vector<AWSet> ds, ss;
     for (int i = 0; i < 40; ++i) {
@@ -210,6 +244,7 @@ int main() {
     TestAWSetDelta();
     TestVersionVector();
     TestPanicsBecomeErrors();
+    TestRaggedVectors();
     TestBatches();
     std::printf("%s: %d failure(s)\n", failures ? "FAILED" : "ok", failures);
     return failures ? 1 : 0;
