@@ -43,11 +43,13 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level tabl
 COPY_MEASURED_GBS = 6290.0  # float4 copy measured on MI355X (MI355X_MICROARCH.md; SURVEY.md 8d second denominator)
 
 
-def box_probe(eng, dev, nbytes=2 << 30, reps=20):
+def box_probe(eng, dev, nbytes=2 << 30, reps=10):
     """This box's own HBM ceiling, measured before any timing (crdt_bw_probe):
-    streaming read, non-temporal write and copy over 2 GiB buffers (8x the
-    256 MiB Infinity Cache), GB/s.  Boxes of one pool differ, so
-    the line states the ceiling of the box that produced it."""
+    streaming read, write and copy over 2 GiB buffers (8x the 256 MiB
+    Infinity Cache), with non-temporal and plain stores and 8/16/32
+    workgroups per CU; each ceiling is the best variant, GB/s.  Boxes of one
+    pool differ, so the line states the ceiling of the box that
+    produced it."""
     import torch
 
     from crdtgpu import abi
@@ -56,14 +58,24 @@ def box_probe(eng, dev, nbytes=2 << 30, reps=20):
     b = torch.empty(nbytes, dtype=torch.uint8, device=dev)
     a.fill_(0x5A)
     torch.cuda.synchronize()
-    out = {"bytes": nbytes, "reps": reps,
-           "read_gbs": eng.bw_probe(abi.CRDT_PROBE_READ, a, b, nbytes, reps),
-           "write_gbs": eng.bw_probe(abi.CRDT_PROBE_WRITE, None, b, nbytes, reps),
-           "copy_gbs": eng.bw_probe(abi.CRDT_PROBE_COPY, a, b, nbytes, reps)}
+    kinds = {"read": abi.CRDT_PROBE_READ, "write_nt": abi.CRDT_PROBE_WRITE, "write_plain": abi.CRDT_PROBE_WRITE_PLAIN,
+             "copy_nt": abi.CRDT_PROBE_COPY, "copy_plain": abi.CRDT_PROBE_COPY_PLAIN}
+    variants = {}
+    for bpc in (8, 16, 32):
+        eng.set_option("probe_blocks_per_cu", bpc)
+        for name, kind in kinds.items():
+            src = None if name.startswith("write") else a
+            variants["%s@%d" % (name, bpc)] = eng.bw_probe(kind, src, b, nbytes, reps)
+    eng.set_option("probe_blocks_per_cu", 16)
     del a, b
     torch.cuda.synchronize()
     torch.cuda.empty_cache()
-    return out
+
+    def best(prefix):
+        return max(v for k, v in variants.items() if k.startswith(prefix))
+
+    return {"bytes": nbytes, "reps": reps, "read_gbs": best("read"), "write_gbs": best("write"),
+            "copy_gbs": best("copy"), "variants": variants}
 
 
 def _np_copy(t, n, dt):
@@ -700,8 +712,8 @@ def main():
     result.update(head)
     if box:
         result["box_probe"] = dict(box, what="crdt_bw_probe on this box before timing: streaming read (16 B/lane), "
-                                             "non-temporal write, copy (read+write bytes); roofline.frac_vs_box = "
-                                             "achieved / copy_gbs")
+                                             "write and copy (read+write bytes), best of nt/plain stores and 8/16/32 "
+                                             "workgroups per CU; roofline.frac_vs_box = achieved / copy_gbs")
     if legs:
         result["legs"] = {}
         for c in legs:

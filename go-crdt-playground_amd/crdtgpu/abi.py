@@ -37,6 +37,8 @@ CRDT_MAX_OPS_PER_DOC = 256
 CRDT_PROBE_READ = 0
 CRDT_PROBE_WRITE = 1
 CRDT_PROBE_COPY = 2
+CRDT_PROBE_WRITE_PLAIN = 3
+CRDT_PROBE_COPY_PLAIN = 4
 
 _vp = ctypes.c_void_p
 _u32 = ctypes.c_uint32

@@ -51,7 +51,8 @@ hipError_t launch_gen_replicas(uint64_t seed, uint32_t n_docs, uint32_t P, uint3
 hipError_t launch_gen_zipf(uint64_t seed, uint32_t n_docs, const uint32_t* offsets, const OutView& A,
                            const OutView& B, hipStream_t stream);
 uint32_t host_zipf_doc_size(uint64_t seed, uint32_t d);
-hipError_t launch_probe(int kind, const void* a, void* b, size_t n16, uint32_t n_cu, hipStream_t stream);
+hipError_t launch_probe(int kind, const void* a, void* b, size_t n16, uint32_t n_cu, uint32_t blocks_per_cu,
+                        hipStream_t stream);
 }  // namespace crdt
 
 using namespace crdt;
@@ -115,6 +116,7 @@ struct crdt_ctx {
     uint32_t max_doc_entries = 0xFFFFFFFFu;  // caller's promise (crdt_ctx_set_max_doc_entries)
     uint32_t join_docs_per_wave = 8;          // crdt_ctx_set_option("join_docs_per_wave")
     bool join_nt_stores = true;               // crdt_ctx_set_option("join_nt_stores")
+    uint32_t probe_blocks_per_cu = 16;        // crdt_ctx_set_option("probe_blocks_per_cu")
     // staging for the *_batch host path
     DevBuf stage[32];
     hipStream_t stream = nullptr;
@@ -337,6 +339,11 @@ int crdt_ctx_set_option(crdt_ctx* ctx, const char* name, int64_t value) {
     }
     if (!strcmp(name, "join_tiles")) {  // 0: large documents one workgroup each (join_block_kernel)
         ctx->join_tiles = value != 0;
+        return CRDT_OK;
+    }
+    if (!strcmp(name, "probe_blocks_per_cu")) {
+        if (value < 1 || value > 64) return CRDT_E_INVALID;
+        ctx->probe_blocks_per_cu = (uint32_t)value;
         return CRDT_OK;
     }
     if (!strcmp(name, "join_nt_stores")) {
@@ -586,8 +593,8 @@ int crdt_gen_zipf_async(crdt_ctx* ctx, uint64_t seed, uint32_t n_docs, const uin
 }
 
 int crdt_bw_probe(crdt_ctx* ctx, int kind, const void* a, void* b, size_t bytes, int reps, double* gbs) {
-    if (!ctx || !gbs || kind < CRDT_PROBE_READ || kind > CRDT_PROBE_COPY || reps < 1 || bytes < 16 || !b ||
-        (kind != CRDT_PROBE_WRITE && !a))
+    if (!ctx || !gbs || kind < CRDT_PROBE_READ || kind > CRDT_PROBE_COPY_PLAIN || reps < 1 || bytes < 16 || !b ||
+        (kind != CRDT_PROBE_WRITE && kind != CRDT_PROBE_WRITE_PLAIN && !a))
         return CRDT_E_INVALID;
     int rc = set_device(ctx);
     if (rc != CRDT_OK) return rc;
@@ -600,9 +607,10 @@ int crdt_bw_probe(crdt_ctx* ctx, int kind, const void* a, void* b, size_t bytes,
     rc = hip_err(hipEventCreate(&e0));
     if (rc == CRDT_OK) rc = hip_err(hipEventCreate(&e1));
     // one untimed launch (first touch, clocks up), then reps timed back to back
-    if (rc == CRDT_OK) rc = hip_err(launch_probe(kind, a, b, n16, (uint32_t)ctx->n_cu, s));
+    if (rc == CRDT_OK) rc = hip_err(launch_probe(kind, a, b, n16, (uint32_t)ctx->n_cu, ctx->probe_blocks_per_cu, s));
     if (rc == CRDT_OK) rc = hip_err(hipEventRecord(e0, s));
-    for (int r = 0; r < reps && rc == CRDT_OK; ++r) rc = hip_err(launch_probe(kind, a, b, n16, (uint32_t)ctx->n_cu, s));
+    for (int r = 0; r < reps && rc == CRDT_OK; ++r)
+        rc = hip_err(launch_probe(kind, a, b, n16, (uint32_t)ctx->n_cu, ctx->probe_blocks_per_cu, s));
     if (rc == CRDT_OK) rc = hip_err(hipEventRecord(e1, s));
     if (rc == CRDT_OK) rc = hip_err(hipEventSynchronize(e1));
     float ms = 0.f;
@@ -610,7 +618,7 @@ int crdt_bw_probe(crdt_ctx* ctx, int kind, const void* a, void* b, size_t bytes,
     if (e0) (void)hipEventDestroy(e0);
     if (e1) (void)hipEventDestroy(e1);
     if (rc == CRDT_OK) {
-        const double moved = (double)n16 * 16.0 * (kind == CRDT_PROBE_COPY ? 2.0 : 1.0);
+        const double moved = (double)n16 * 16.0 * ((kind == CRDT_PROBE_COPY || kind == CRDT_PROBE_COPY_PLAIN) ? 2.0 : 1.0);
         *gbs = ms > 0.f ? moved * reps / (ms * 1e-3) / 1e9 : 0.0;
     }
     return leave(ctx, s, cap, rc);

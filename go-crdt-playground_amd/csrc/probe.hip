@@ -25,37 +25,53 @@ __global__ __launch_bounds__(256) void probe_read_kernel(const u32x4* __restrict
     if (acc.x == 0x9E3779B9u && acc.y == 0x7F4A7C15u) sink[0] = acc.z ^ acc.w;
 }
 
+template <bool NT>
+__device__ __forceinline__ void put16(u32x4 v, u32x4* p) {
+    if (NT)
+        __builtin_nontemporal_store(v, p);
+    else
+        *p = v;
+}
+
+template <bool NT>
 __global__ __launch_bounds__(256) void probe_write_kernel(u32x4* __restrict__ b, size_t n) {
     const size_t stride = (size_t)gridDim.x * blockDim.x;
     for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += stride) {
         const u32x4 v = {(uint32_t)i, (uint32_t)(i >> 32), 0x5EEDu, 1u};
-        __builtin_nontemporal_store(v, b + i);
+        put16<NT>(v, b + i);
     }
 }
 
+template <bool NT>
 __global__ __launch_bounds__(256) void probe_copy_kernel(const u32x4* __restrict__ a, u32x4* __restrict__ b,
                                                          size_t n) {
     const size_t stride = (size_t)gridDim.x * blockDim.x;
     size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
     for (; i + 3 * stride < n; i += 4 * stride) {
         const u32x4 x0 = a[i], x1 = a[i + stride], x2 = a[i + 2 * stride], x3 = a[i + 3 * stride];
-        __builtin_nontemporal_store(x0, b + i);
-        __builtin_nontemporal_store(x1, b + i + stride);
-        __builtin_nontemporal_store(x2, b + i + 2 * stride);
-        __builtin_nontemporal_store(x3, b + i + 3 * stride);
+        put16<NT>(x0, b + i);
+        put16<NT>(x1, b + i + stride);
+        put16<NT>(x2, b + i + 2 * stride);
+        put16<NT>(x3, b + i + 3 * stride);
     }
-    for (; i < n; i += stride) __builtin_nontemporal_store(a[i], b + i);
+    for (; i < n; i += stride) put16<NT>(a[i], b + i);
 }
 
-// kind 0 read a, 1 write b, 2 copy a -> b; n16 = 16-byte words.
-hipError_t launch_probe(int kind, const void* a, void* b, size_t n16, uint32_t n_cu, hipStream_t stream) {
-    const uint32_t grid = n_cu * 16u;
-    if (kind == 0)
-        hipLaunchKernelGGL(probe_read_kernel, dim3(grid), dim3(256), 0, stream, (const u32x4*)a, n16, (uint32_t*)b);
-    else if (kind == 1)
-        hipLaunchKernelGGL(probe_write_kernel, dim3(grid), dim3(256), 0, stream, (u32x4*)b, n16);
-    else
-        hipLaunchKernelGGL(probe_copy_kernel, dim3(grid), dim3(256), 0, stream, (const u32x4*)a, (u32x4*)b, n16);
+// kind (crdtgpu.h CRDT_PROBE_*): 0 read a, 1 write b (nt), 2 copy a -> b (nt),
+// 3 write b (plain stores), 4 copy (plain stores); n16 = 16-byte words;
+// blocks_per_cu workgroups of 256 threads per CU.
+hipError_t launch_probe(int kind, const void* a, void* b, size_t n16, uint32_t n_cu, uint32_t blocks_per_cu,
+                        hipStream_t stream) {
+    const uint32_t grid = n_cu * blocks_per_cu;
+    const u32x4* src = (const u32x4*)a;
+    u32x4* dst = (u32x4*)b;
+    switch (kind) {
+        case 0: hipLaunchKernelGGL(probe_read_kernel, dim3(grid), dim3(256), 0, stream, src, n16, (uint32_t*)b); break;
+        case 1: hipLaunchKernelGGL(probe_write_kernel<true>, dim3(grid), dim3(256), 0, stream, dst, n16); break;
+        case 2: hipLaunchKernelGGL(probe_copy_kernel<true>, dim3(grid), dim3(256), 0, stream, src, dst, n16); break;
+        case 3: hipLaunchKernelGGL(probe_write_kernel<false>, dim3(grid), dim3(256), 0, stream, dst, n16); break;
+        default: hipLaunchKernelGGL(probe_copy_kernel<false>, dim3(grid), dim3(256), 0, stream, src, dst, n16); break;
+    }
     return hipGetLastError();
 }
 

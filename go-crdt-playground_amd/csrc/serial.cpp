@@ -13,6 +13,7 @@
 #include <cstdint>
 #include <cstring>
 #include <string>
+#include <vector>
 
 #include "../../include/crdtgpu.h"
 
@@ -204,7 +205,9 @@ int crdt_batch_dump(const crdt_awset_batch* b, void* buf, size_t cap, size_t* le
     *len = need;
     if (!buf) return CRDT_OK;
     if (cap < need) return CRDT_E_CAPACITY;
-    unsigned char* p = (unsigned char*)buf;
+    // built in an aligned scratch image, then copied: buf may sit at any address
+    std::vector<uint64_t> img((need + 7) / 8);
+    unsigned char* p = (unsigned char*)img.data();
     memcpy(p, kMagic, 8);
     memcpy(p + 8, &b->n_docs, 4);
     memcpy(p + 12, &b->R, 4);
@@ -229,6 +232,7 @@ int crdt_batch_dump(const crdt_awset_batch* b, void* buf, size_t cap, size_t* le
     memcpy(vv, b->vv, 8 * (size_t)b->n_docs * b->R);
     const uint64_t h = fnv1a(p, need - 8);
     memcpy(p + need - 8, &h, 8);
+    memcpy(buf, p, need);
     return CRDT_OK;
 }
 
@@ -263,14 +267,19 @@ int crdt_batch_undump(const void* buf, size_t len, const crdt_awset_out* out) {
         (nd && !out->vv))
         return CRDT_E_INVALID;
     const unsigned char* p = (const unsigned char*)buf;
-    const uint32_t* off = (const uint32_t*)(p + kHeader);
+    const unsigned char* off = p + kHeader;  // u32 array; the image may sit at any address: memcpy reads
     const unsigned char* q = p + kHeader + offs_bytes(nd);
-    if (off[0] != 0) return CRDT_E_INVALID;
+    auto off_at = [off](uint32_t d) {
+        uint32_t v;
+        memcpy(&v, off + 4 * (size_t)d, 4);
+        return v;
+    };
+    if (off_at(0) != 0) return CRDT_E_INVALID;
     for (uint32_t d = 0; d < nd; ++d)
-        if (off[d + 1] < off[d] || off[d + 1] > n) return CRDT_E_INVALID;
-    if (off[nd] != n) return CRDT_E_INVALID;
+        if (off_at(d + 1) < off_at(d) || off_at(d + 1) > n) return CRDT_E_INVALID;
+    if (off_at(nd) != n) return CRDT_E_INVALID;
     memcpy(out->offsets, off, 4 * ((size_t)nd + 1));
-    for (uint32_t d = 0; d < nd; ++d) out->counts[d] = off[d + 1] - off[d];
+    for (uint32_t d = 0; d < nd; ++d) out->counts[d] = off_at(d + 1) - off_at(d);
     memcpy(out->keys, q, 8 * n);
     memcpy(out->counters, q + 8 * n, 8 * n);
     memcpy(out->actors, q + 16 * n, 4 * n);

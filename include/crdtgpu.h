@@ -155,7 +155,10 @@ int crdt_ctx_reserve(crdt_ctx* ctx, uint32_t max_docs, uint64_t max_fold_slots);
 int crdt_ctx_set_max_doc_entries(crdt_ctx* ctx, uint32_t max_entries);
 /* Tuning knobs (performance only, never results):
  *   "join_docs_per_wave"  1|2|4|8|16  documents one wavefront pipelines (default 8)
- *   "join_nt_stores"      0|1         non-temporal output stores (default 1) */
+ *   "join_nt_stores"      0|1         non-temporal output stores (default 1)
+ *   "probe_blocks_per_cu" 1..64       crdt_bw_probe grid (default 16)
+ *   (also "join_tile_capacity", "join_tile_shape", "join_tile_nt_stores",
+ *   "join_tiles": see api.cpp) */
 int crdt_ctx_set_option(crdt_ctx* ctx, const char* name, int64_t value);
 /* Wait for `stream`, return (and clear) the first device-side error. */
 int crdt_ctx_sync(crdt_ctx* ctx, void* stream);
@@ -209,12 +212,16 @@ int crdt_gen_replicas_async(crdt_ctx* ctx, uint64_t seed, uint32_t n_docs, uint3
  * Times `reps` launches of a streaming kernel over caller-owned device memory
  * on the context's stream (after one untimed launch) and returns the HBM rate
  * in GB/s (1e9 B/s): READ reads `bytes` of a (16 B per lane, four loads in
- * flight), WRITE writes `bytes` to b (16 B non-temporal stores), COPY reads a
- * and writes b (counts 2 x bytes).  READ needs b as a 4-byte sink.  Use
- * buffers well above the 256 MiB Infinity Cache.  Synchronous. */
+ * flight), WRITE writes `bytes` to b (16 B non-temporal stores; _PLAIN: plain
+ * stores), COPY reads a and writes b (counts 2 x bytes).  READ needs b as a
+ * 4-byte sink.  Grid: crdt_ctx_set_option("probe_blocks_per_cu", 1..64,
+ * default 16) workgroups of 256 per CU.  Use buffers well above the 256 MiB
+ * Infinity Cache.  Synchronous. */
 #define CRDT_PROBE_READ 0
 #define CRDT_PROBE_WRITE 1
 #define CRDT_PROBE_COPY 2
+#define CRDT_PROBE_WRITE_PLAIN 3
+#define CRDT_PROBE_COPY_PLAIN 4
 int crdt_bw_probe(crdt_ctx* ctx, int kind, const void* a, void* b, size_t bytes, int reps, double* gbs);
 
 /* ---- batched local operations: the state producers -----

@@ -112,3 +112,24 @@ def batch_of(R, docs, slack=0):
 
 def src_batch_of(R, per_doc):
     return SrcBatch.from_lists(R, per_doc)
+
+
+def config1_history(rng: random.Random, delta: bool, n_base: int = 1000):
+    """two replicas A (actor 0) and B (actor 1) of one
+    reachable ~1,000-element document.  A adds n_base keys, B merges A; then
+    each side independently deletes 10 % of the base keys, adds 10 % new keys
+    and re-adds 5 % (half of its deletes), with the reference's own ops
+    (awset.go:89-101, awset-delta_test.go:14-33).  Returns (A, B) of the map
+    restatement (oracle/awset_ref.py)."""
+    cls = ref.AWSetDelta if delta else ref.AWSet
+    A, B = cls(0, ref.VersionVector([0, 0])), cls(1, ref.VersionVector([0, 0]))
+    base = ["e%04d" % i for i in range(n_base)]
+    A.Add(*base)
+    B.Merge(A)
+    for r, X in enumerate((A, B)):
+        gone = rng.sample(base, n_base // 10)
+        for i in range(0, len(gone), 7):  # several Del calls (AWSetDelta.Del bumps once per call)
+            X.Del(*gone[i:i + 7])
+        X.Add(*["n%d_%04d" % (r, i) for i in range(n_base // 10)])
+        X.Add(*rng.sample(gone, n_base // 20))
+    return A, B

@@ -294,3 +294,57 @@ def test_ragged_version_vectors_match_reference(kind):
     with pytest.raises(CrdtError) as ei:
         MergeBatch([a], [b])
     assert ei.value.code == abi.CRDT_E_INVALID
+
+
+def _mirror_of(x):
+    """map-restatement state -> Python-mirror state (same actor, clock, maps)."""
+    m = (AWSetDelta if hasattr(x, "Deleted") else AWSet)(x.Actor, list(x.VersionVector),
+                                                          {k: Dot(d.actor, d.counter) for k, d in x.Entries.items()})
+    if hasattr(x, "Deleted") and x.Deleted is not None:
+        m.Deleted = {k: Dot(d.actor, d.counter) for k, d in x.Deleted.items()}
+    return m
+
+
+def _same(m, x):
+    assert {k: (d.Actor, d.Counter) for k, d in m.Entries.items()} == \
+        {k: (d.actor, d.counter) for k, d in x.Entries.items()}
+    assert list(m.VersionVector) == list(x.VersionVector)
+
+
+@pytest.mark.parametrize("delta", [False, True])
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_config1_two_replica_history(delta, seed):
+    """BASELINE config 1 on the GPU, as SURVEY.md 8d states it: a reachable
+    1,000-element two-replica history (each side deletes 10 %, adds 10 % new
+    keys, re-adds 5 %), merged both ways, full-state (AWSet) and AWSetDelta:
+      * the two merges of one snapshot, x = A<-B and y = B<-A, in one batch;
+      * the reference's sequential round trip A.Merge(B); B.Merge(A)
+        (awset_test.go:15-16), each merge one GPU call.
+    Exact vs the map restatement of the reference: element sets, dots, clocks."""
+    import random
+
+    from helpers import config1_history
+
+    A, B = config1_history(random.Random(seed), delta)
+    assert 1000 <= len(A.Entries) <= 1100 and A.Entries != B.Entries
+    merge = DeltaMergeBatch if delta else None
+    # two merges of one snapshot
+    x, y = A.Clone(), B.Clone()
+    x.Merge(B)
+    y.Merge(A)
+    mx, my = _mirror_of(A), _mirror_of(B)
+    if delta:
+        merge([mx, my], [[_mirror_of(B)], [_mirror_of(A)]])
+    else:
+        MergeBatch([mx, my], [_mirror_of(B), _mirror_of(A)])
+    _same(mx, x)
+    _same(my, y)
+    # sequential round trip: the second merge sees the merged A
+    ma, mb = _mirror_of(A), _mirror_of(B)
+    A.Merge(B)
+    B.Merge(A)
+    ma.Merge(mb)
+    mb.Merge(ma)
+    _same(ma, A)
+    _same(mb, B)
+    assert sorted(A.Entries) == sorted(B.Entries)  # converged element sets

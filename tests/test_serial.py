@@ -104,3 +104,22 @@ def test_dump_rejects_corruption():
     empty = AWSetBatch(2, np.zeros(1, np.uint32), np.zeros(1, np.uint64), np.zeros(1, np.uint32),
                        np.zeros(1, np.uint64), np.zeros(1, np.uint64))
     assert crdtgpu.load_batch(crdtgpu.dump_batch(empty)).n_docs == 0
+
+
+def test_image_parser_fuzz_under_sanitizers():
+    """crdt_batch_info / crdt_batch_undump parse images a caller may not
+    control: tests/cpp/fuzz_serial.cpp mutates dumped images (header fields,
+    offsets, lengths, bytes) and re-signs the checksum so the parser's own
+    checks are what stands between a bad image and the output arrays; images
+    sit at misaligned addresses too.  Built with ASan + UBSan (host code only,
+    host/Makefile build/fuzz_serial): any report aborts with a non-zero exit."""
+    import os
+    import subprocess
+
+    exe = os.path.join(os.path.dirname(crdtgpu.__file__), "..", "host", "build", "fuzz_serial")
+    if not os.path.exists(exe):
+        subprocess.check_call(["make", "-s", "-C", os.path.dirname(os.path.dirname(exe)), "build/fuzz_serial"])
+    for seed in (1, 2, 3):
+        r = subprocess.run([exe, "30000", str(seed)], capture_output=True, text=True, timeout=120)
+        assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+        assert r.stdout.startswith("ok:"), r.stdout
