@@ -612,10 +612,13 @@ def run_config(config, n, args, ctx, steps, warmup, repeats, cpu, box=None):
 
 
 def boundary_cost(n_docs):
-    """the host side of the drop-in, phase by phase (string
-    interning, SoA pack, H2D, exchange kernel, D2H, unpack to map[string]Dot),
-    through the C++ host mirror (tests/cpp/boundary_bench.cpp) on config-2-shaped
-    docs.  Never part of `value` (inputs there are already resident in HBM)."""
+    """the host side of the drop-in, phase by phase, through
+    the C++ host mirror's ExchangeBatch (tests/cpp/boundary_bench.cpp):
+    pack (hash interning with an exact per-document collision check, entries
+    sorted into page-locked SoA), device (H2D + exchange + D2H), apply (results
+    applied to the maps in place), next to the reference merge on the same maps
+    on every host thread.  Never part of `value` (inputs there are already
+    resident in HBM)."""
     import subprocess
 
     exe = os.path.join(ROOT, "go-crdt-playground_amd", "host", "build", "boundary_bench")
@@ -624,11 +627,12 @@ def boundary_cost(n_docs):
     try:
         r = subprocess.run([exe, str(n_docs)], capture_output=True, text=True, timeout=300)
         if r.returncode != 0:
-            return {"error": "exit %d: %s" % (r.returncode, r.stderr[-300:])}
+            return {"error": "exit %d: %s" % (r.returncode, (r.stdout + r.stderr)[-300:])}
         out = json.loads(r.stdout.strip().splitlines()[-1])
-        out["what"] = ("C++ host mirror (go-crdt-playground_amd/host/crdt.hpp) around one exchange call: string keys "
-                       "interned to order-preserving ids, packed to SoA, copied H2D (pageable), both merges, D2H, "
-                       "rebuilt as unordered_map<string,Dot>; config-2-shaped docs")
+        out["what"] = ("C++ host mirror (go-crdt-playground_amd/host/crdt.hpp) ExchangeBatch: map[string]Dot-shaped "
+                       "states in, both merges of every doc, the same maps updated in place; config-2-shaped docs "
+                       "with 12-16 byte string keys; cpu_same_states = the reference merge on the same maps, every "
+                       "host thread")
         return out
     except Exception as e:  # reported, never fatal to the bench line
         return {"error": "%s: %s" % (type(e).__name__, e)}

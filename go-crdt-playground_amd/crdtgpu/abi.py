@@ -147,6 +147,8 @@ def _load():
         "crdt_awset_fold_batch": (ctypes.c_int, [_vp, ctypes.c_int, P(CAWSetBatch), P(CSrcBatch), P(CAWSetOut)]),
         "crdt_bw_probe": (ctypes.c_int, [_vp, ctypes.c_int, _vp, _vp, ctypes.c_size_t, ctypes.c_int,
                                          P(ctypes.c_double)]),
+        "crdt_host_alloc": (ctypes.c_int, [ctypes.c_size_t, P(_vp)]),
+        "crdt_host_free": (None, [_vp]),
         "crdt_validate_batch": (ctypes.c_int, [P(CAWSetBatch)]),
         "crdt_validate_src_batch": (ctypes.c_int, [P(CSrcBatch)]),
         "crdt_validate_tomb_batch": (ctypes.c_int, [P(CTombBatch), _u32]),

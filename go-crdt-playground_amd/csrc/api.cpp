@@ -624,6 +624,17 @@ int crdt_bw_probe(crdt_ctx* ctx, int kind, const void* a, void* b, size_t bytes,
     return leave(ctx, s, cap, rc);
 }
 
+int crdt_host_alloc(size_t bytes, void** out) {
+    if (!out) return CRDT_E_INVALID;
+    *out = nullptr;
+    if (bytes == 0) bytes = 1;
+    return hipHostMalloc(out, bytes, hipHostMallocDefault) == hipSuccess ? CRDT_OK : CRDT_E_NOMEM;
+}
+
+void crdt_host_free(void* p) {
+    if (p) (void)hipHostFree(p);
+}
+
 /* ---------------- validation (host) ---------------- */
 
 int crdt_validate_batch(const crdt_awset_batch* b) {

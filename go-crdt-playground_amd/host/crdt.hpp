@@ -5,12 +5,22 @@
 //   VersionVector                     crdt-misc.go:21-74
 //   AWSet                             awset.go:55-171
 //   AWSetDelta                        awset-delta_test.go:9-77
-// Merge() and the batch entry points (MergeBatch, FoldBatch, DeltaMergeBatch)
-// intern the string keys of each document into order-preserving u64 ids (the
-// ranks of the document's keys; host work spread over threads), pack the
-// structure-of-arrays buffers of include/crdtgpu.h, run the HIP kernels through
-// crdt_awset_join_batch / crdt_awset_fold_batch and unpack the result.  Local
-// ops (Add, Del, Clone, ...) are per-replica host state, as in the reference.
+// Merge() and the batch entry points (MergeBatch, ExchangeBatch, FoldBatch,
+// DeltaMergeBatch) move map[string]Dot-shaped states through the C ABI
+// (include/crdtgpu.h) and back, per document on host threads:
+//   intern  each key -> a 64-bit hash id; a document whose states hold two
+//           different keys with one id (checked exactly, by string compare on
+//           equal ids) falls back to rank ids (its keys' ranks in string
+//           order), so ids are always an exact bijection per document
+//   pack    entries sorted by id straight into page-locked SoA arrays
+//           (crdt_host_alloc, kept by the Engine and reused across calls)
+//   merge   crdt_awset_join_batch / _exchange_batch / _fold_batch
+//   apply   the result applied to each destination map IN PLACE, as the
+//           reference's merge mutates dst.Entries (awset.go:142,154): removed
+//           keys erased, changed dots overwritten, new keys inserted -- no
+//           map is rebuilt
+// Local ops (Add, Del, Clone, ...) are per-replica host state, as in the
+// reference.
 //
 // Where the Go code panics (HasDot/Counter at actor == len(vv), Add with the
 // actor outside the vector), this API throws crdt::Error carrying the C ABI
@@ -25,8 +35,10 @@
 #pragma once
 
 #include <algorithm>
+#include <chrono>
 #include <cstdint>
 #include <cstdlib>
+#include <cstring>
 #include <map>
 #include <stdexcept>
 #include <string>
@@ -93,7 +105,43 @@ struct VersionVector : std::vector<uint64_t> {
 
 using Entries = std::unordered_map<std::string, Dot>;
 
-// One context per host thread (crdt_ctx).
+namespace detail {
+// Page-locked host buffer (crdt_host_alloc), grown on demand, kept for reuse:
+// allocating page-locked memory costs far more than filling it.
+struct PinnedBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+    PinnedBuf() = default;
+    PinnedBuf(const PinnedBuf&) = delete;
+    PinnedBuf& operator=(const PinnedBuf&) = delete;
+    ~PinnedBuf() { crdt_host_free(p); }
+    void* get(size_t want) {
+        want = std::max<size_t>(want, 64);
+        if (want > bytes) {
+            crdt_host_free(p);
+            p = nullptr;
+            bytes = 0;
+            want += want / 8;
+            check(crdt_host_alloc(want, &p), "crdt_host_alloc");
+            bytes = want;
+        }
+        return p;
+    }
+};
+
+// staging roles of one batch call
+enum Pin {
+    kD_OFF, kD_KEY, kD_ACT, kD_CTR, kD_VV,        // destinations
+    kS_OFF, kS_KEY, kS_ACT, kS_CTR, kS_VV,        // sources (join / exchange: one per doc)
+    kS_DOC, kS_SACT, kS_TOFF, kS_TKEY, kS_TACT, kS_TCTR,  // fold sources: doc_srcs, src_actor, tombstones
+    kO_OFF, kO_CNT, kO_KEY, kO_ACT, kO_CTR, kO_VV,  // output
+    kP_OFF, kP_CNT, kP_KEY, kP_ACT, kP_CTR, kP_VV,  // second output (exchange)
+    kPinSlots
+};
+}  // namespace detail
+
+// One context per host thread (crdt_ctx), plus the page-locked staging its
+// batch calls reuse.
 class Engine {
    public:
     explicit Engine(int device = 0) { check(crdt_ctx_create(device, &ctx_), "crdt_ctx_create"); }
@@ -105,9 +153,14 @@ class Engine {
         static thread_local Engine e(0);
         return e;
     }
+    template <typename T>
+    T* pinned(int role, size_t n) {
+        return static_cast<T*>(pin_[role].get(n * sizeof(T)));
+    }
 
    private:
     crdt_ctx* ctx_ = nullptr;
+    detail::PinnedBuf pin_[detail::kPinSlots];
 };
 
 class AWSetDelta;
@@ -180,23 +233,23 @@ class AWSetDelta : public AWSet {
     const Entries* deleted_map() const override { return &deleted; }
 };
 
-namespace detail {
-
-struct Packed {
-    std::vector<uint32_t> offsets{0};
-    std::vector<uint64_t> keys;
-    std::vector<uint32_t> actors;
-    std::vector<uint64_t> counters;
-    std::vector<uint64_t> vv;
+// Seconds per phase of the last batch call on this thread (boundary cost).
+struct BoundaryStats {
+    double pack_s = 0, device_s = 0, apply_s = 0;
+    size_t rank_docs = 0;  // documents interned by rank after a hash collision
 };
-
-template <typename T>
-T* data_or_null(std::vector<T>& v) {
-    return v.empty() ? nullptr : v.data();
+inline BoundaryStats& LastStats() {
+    static thread_local BoundaryStats s;
+    return s;
 }
 
+namespace detail {
+
+using clk = std::chrono::steady_clock;
+inline double secs_since(clk::time_point t) { return std::chrono::duration<double>(clk::now() - t).count(); }
+
 // Worker threads for the per-document host work (interning, packing,
-// unpacking): CRDT_HOST_THREADS, else OMP_NUM_THREADS, else the hardware
+// applying): CRDT_HOST_THREADS, else OMP_NUM_THREADS, else the hardware
 // threads (at most 16); 1 = serial.
 inline unsigned host_threads() {
     static const unsigned n = [] {
@@ -226,111 +279,240 @@ void parallel_docs(size_t n, F&& fn) {
     for (auto& th : pool) th.join();
 }
 
-// Interning + packing shared by the batch entry points.  Keys are interned
-// per document: the merge only ever compares keys of one document, so a
-// document's ids are the ranks of its keys (over every state of that document
-// in the batch) in string order -- an exact, order-preserving bijection per
-// document, as the C ABI requires, built from a small sort per document.
+// 64-bit key hash (8-byte words, multiply-xorshift mixing).  Collisions are
+// detected exactly per document, so the quality only sets how often the rank
+// fallback runs.
+inline uint64_t key_hash(const std::string& s) {
+    const unsigned char* p = (const unsigned char*)s.data();
+    size_t n = s.size();
+    uint64_t h = 0x9E3779B97F4A7C15ull ^ (n * 0xC2B2AE3D27D4EB4Full);
+    while (n >= 8) {
+        uint64_t w;
+        memcpy(&w, p, 8);
+        h = (h ^ w) * 0xFF51AFD7ED558CCDull;
+        h ^= h >> 29;
+        p += 8;
+        n -= 8;
+    }
+    uint64_t w = 0;
+    memcpy(&w, p, n);
+    h = (h ^ w ^ ((uint64_t)n << 56)) * 0xC4CEB9FE1A85EC53ull;
+    h ^= h >> 32;
+    h *= 0xD6E8FEB86659FD93ull;
+    return h ^ (h >> 32);
+}
+
+// CRDT_HOST_RANK_IDS=1: every document takes the collision fallback (tests).
+inline bool force_rank_ids() {
+    static const bool f = [] {
+        const char* e = std::getenv("CRDT_HOST_RANK_IDS");
+        return e && e[0] == '1';
+    }();
+    return f;
+}
+
+// One packed slot: key id, the dot, and the map element it came from (its
+// key string; for a destination, the element the result updates in place).
+struct SlotRef {
+    uint64_t id;
+    Dot dot;
+    Entries::iterator it;
+};
+
+// The states of a batch: role 0 = destinations (one per document), role 1 =
+// the sources (one per document for a join, any number for a fold); each
+// state's slots are contiguous, sorted by id, at first[role][state].
 struct Batch {
     size_t R = 1;
-    std::vector<std::vector<const std::string*>> names;  // doc -> id -> key
+    size_t n_docs = 0;
+    std::vector<AWSet*> dst;                   // [n_docs]
+    std::vector<const AWSet*> src;             // all sources, doc-major
+    std::vector<uint32_t> src_beg{0};          // doc d's sources: [src_beg[d], src_beg[d+1])
+    std::vector<uint32_t> dfirst, sfirst;      // per state: first slot (prefix of entry counts)
+    std::vector<uint32_t> tfirst;              // per source: first tombstone slot
+    std::vector<SlotRef> dref, sref;           // per slot (host side of the SoA)
+    std::vector<uint8_t> rank_doc;             // 1: ids of doc d are ranks (hash collision)
+};
 
-    // doc d's states: every key of each (entries and Deleted) becomes an id
-    void intern(size_t d, const std::vector<const AWSet*>& states) {
-        auto& v = names[d];
-        v.clear();
-        for (auto* s : states) {
-            for (auto& kv : s->entries) v.push_back(&kv.first);
-            if (auto* del = s->deleted_map())
-                for (auto& kv : *del) v.push_back(&kv.first);
-        }
-        std::sort(v.begin(), v.end(), [](const std::string* a, const std::string* b) { return *a < *b; });
-        v.erase(std::unique(v.begin(), v.end(), [](const std::string* a, const std::string* b) { return *a == *b; }),
-                v.end());
-    }
-    uint64_t id(size_t d, const std::string& k) const {
-        const auto& v = names[d];
-        return (uint64_t)(std::lower_bound(v.begin(), v.end(), &k,
-                                           [](const std::string* a, const std::string* b) { return *a < *b; }) -
-                          v.begin());
-    }
-    // write map m of doc d at k/a/c[at..], sorted by id
-    void put_entries(size_t d, const Entries& m, uint64_t* k, uint32_t* a, uint64_t* c) const {
-        std::vector<std::pair<uint64_t, Dot>> v;
-        v.reserve(m.size());
-        for (auto& kv : m) v.emplace_back(id(d, kv.first), kv.second);
-        std::sort(v.begin(), v.end(), [](auto& x, auto& y) { return x.first < y.first; });
-        for (size_t i = 0; i < v.size(); ++i) {
-            k[i] = v[i].first;
-            a[i] = v[i].second.actor;
-            c[i] = v[i].second.counter;
+// Fill doc d's slots: ids (hash, or ranks after a collision), sorted per
+// state, written to the page-locked SoA arrays and to the SlotRef arrays.
+struct DocPacker {
+    Batch& b;
+    uint64_t *dk, *sk, *tk, *dc, *sc, *tc;
+    uint32_t *da, *sa, *ta;
+    std::vector<std::pair<uint64_t, const std::string*>> names;  // thread-local scratch
+    std::vector<const std::string*> sorted;                      // rank fallback scratch
+    std::vector<SlotRef> tmp;
+
+    bool collect = false;  // hash pass: note (id, key) of every slot for the exact check
+
+    template <typename IdOf>
+    void put_state(const Entries& m, uint32_t first, uint64_t* k, uint32_t* a, uint64_t* c, SlotRef* ref, IdOf&& id_of) {
+        tmp.clear();
+        for (auto it = const_cast<Entries&>(m).begin(); it != m.end(); ++it) tmp.push_back(SlotRef{id_of(it->first), it->second, it});
+        std::sort(tmp.begin(), tmp.end(), [](const SlotRef& x, const SlotRef& y) { return x.id < y.id; });
+        for (size_t i = 0; i < tmp.size(); ++i) {
+            k[first + i] = tmp[i].id;
+            a[first + i] = tmp[i].dot.actor;
+            c[first + i] = tmp[i].dot.counter;
+            if (ref) ref[first + i] = tmp[i];
+            if (collect) names.emplace_back(tmp[i].id, &tmp[i].it->first);
         }
     }
-    // one state per doc (states[d] of doc d), offsets = prefix of entry counts
-    Packed pack(const std::vector<AWSet*>& states) const {
-        Packed p;
-        const size_t n = states.size();
-        p.offsets.assign(n + 1, 0);
-        for (size_t d = 0; d < n; ++d) p.offsets[d + 1] = p.offsets[d] + (uint32_t)states[d]->entries.size();
-        const size_t tot = p.offsets[n];
-        p.keys.resize(tot);
-        p.actors.resize(tot);
-        p.counters.resize(tot);
-        p.vv.assign(n * R, 0);
-        parallel_docs(n, [&](size_t lo, size_t hi) {
-            for (size_t d = lo; d < hi; ++d) {
-                const uint32_t o = p.offsets[d];
-                put_entries(d, states[d]->entries, p.keys.data() + o, p.actors.data() + o, p.counters.data() + o);
-                const auto& v = states[d]->versionVector;
-                for (size_t r = 0; r < std::min(R, v.size()); ++r) p.vv[d * R + r] = v[r];
-            }
-        });
-        return p;
+    template <typename IdOf>
+    void put_doc(size_t d, IdOf&& id_of) {
+        put_state(b.dst[d]->entries, b.dfirst[d], dk, da, dc, b.dref.data(), id_of);
+        for (uint32_t s = b.src_beg[d]; s < b.src_beg[d + 1]; ++s) {
+            put_state(b.src[s]->entries, b.sfirst[s], sk, sa, sc, b.sref.data(), id_of);
+            if (tk)
+                if (auto* del = b.src[s]->deleted_map()) put_state(*del, b.tfirst[s], tk, ta, tc, nullptr, id_of);
+        }
     }
-    crdt_awset_batch view(Packed& p) const {
-        return crdt_awset_batch{(uint32_t)(p.offsets.size() - 1), (uint32_t)R, p.offsets.data(), nullptr,
-                                data_or_null(p.keys), data_or_null(p.actors), data_or_null(p.counters),
-                                data_or_null(p.vv)};
-    }
-    void unpack(const std::vector<AWSet*>& dsts, const Packed& out, const std::vector<uint32_t>& counts,
-                const std::vector<size_t>& widths) const {
-        parallel_docs(dsts.size(), [&](size_t lo, size_t hi) {
-            for (size_t d = lo; d < hi; ++d) {
-                Entries m;
-                m.reserve(counts[d]);
-                for (uint32_t j = out.offsets[d]; j < out.offsets[d] + counts[d]; ++j)
-                    m.emplace(*names[d][out.keys[j]], Dot{out.actors[j], out.counters[j]});
-                dsts[d]->entries = std::move(m);
-                VersionVector vv(widths[d]);
-                for (size_t r = 0; r < widths[d]; ++r) vv[r] = out.vv[d * R + r];
-                dsts[d]->versionVector = std::move(vv);
-            }
+    void doc(size_t d) {
+        names.clear();
+        collect = true;
+        put_doc(d, [](const std::string& k) { return key_hash(k); });
+        collect = false;
+        // exact check: equal ids must be equal strings, over every state of the doc
+        std::sort(names.begin(), names.end(), [](const auto& x, const auto& y) { return x.first < y.first; });
+        bool clash = force_rank_ids();
+        for (size_t i = 1; i < names.size() && !clash; ++i)
+            clash = names[i].first == names[i - 1].first && *names[i].second != *names[i - 1].second;
+        if (!clash) return;
+        // rank ids: the key's rank in string order over the doc's states
+        b.rank_doc[d] = 1;
+        sorted.clear();
+        for (auto& x : names) sorted.push_back(x.second);
+        auto lt = [](const std::string* x, const std::string* y) { return *x < *y; };
+        std::sort(sorted.begin(), sorted.end(), lt);
+        sorted.erase(std::unique(sorted.begin(), sorted.end(), [](auto* x, auto* y) { return *x == *y; }), sorted.end());
+        put_doc(d, [&](const std::string& k) {
+            return (uint64_t)(std::lower_bound(sorted.begin(), sorted.end(), &k, lt) - sorted.begin());
         });
     }
 };
 
-inline Packed make_out(size_t n_docs, size_t R, size_t slots, std::vector<uint32_t>& counts, crdt_awset_out& o) {
-    Packed p;
-    p.offsets.assign(n_docs + 1, 0);
-    p.keys.assign(slots + 1, 0);
-    p.actors.assign(slots + 1, 0);
-    p.counters.assign(slots + 1, 0);
-    p.vv.assign(std::max<size_t>(n_docs * R, 1), 0);
-    counts.assign(std::max<size_t>(n_docs, 1), 0);
-    o = crdt_awset_out{p.offsets.data(), counts.data(), p.keys.data(), p.actors.data(), p.counters.data(), p.vv.data()};
-    return p;
+// Slot counts and offsets of every state (serial: prefix sums).
+inline void layout(Batch& b, bool tombs) {
+    b.dfirst.assign(b.n_docs + 1, 0);
+    for (size_t d = 0; d < b.n_docs; ++d) b.dfirst[d + 1] = b.dfirst[d] + (uint32_t)b.dst[d]->entries.size();
+    const size_t ns = b.src.size();
+    b.sfirst.assign(ns + 1, 0);
+    b.tfirst.assign(ns + 1, 0);
+    for (size_t s = 0; s < ns; ++s) {
+        b.sfirst[s + 1] = b.sfirst[s] + (uint32_t)b.src[s]->entries.size();
+        const Entries* del = tombs ? b.src[s]->deleted_map() : nullptr;
+        b.tfirst[s + 1] = b.tfirst[s] + (uint32_t)(del ? del->size() : 0);
+    }
+    if ((uint64_t)b.dfirst[b.n_docs] + b.sfirst[ns] >= (1ull << 32)) throw Error(CRDT_E_INVALID, "batch too large");
+    b.dref.resize(b.dfirst[b.n_docs]);
+    b.sref.resize(b.sfirst[ns]);
+    b.rank_doc.assign(b.n_docs, 0);
 }
 
-// Intern a batch: doc d's states are states_of(d).
-template <typename F>
-void intern_all(Batch& b, size_t n, F&& states_of) {
-    b.names.assign(n, {});
+// The merged doc (out entries [o, o + c), sorted by id) applied to its
+// destination map in place, as the reference's merge mutates dst.Entries:
+// keys absent from the result are erased, dots that differ are overwritten,
+// new keys inserted -- their strings come from the sources' elements.  plan()
+// only reads (the iterators taken when packing are still valid); commit()
+// erases, overwrites, then inserts.
+struct Plan {
+    std::vector<Entries::iterator> erase;
+    std::vector<std::pair<Entries::iterator, Dot>> upd;
+    std::vector<std::pair<const std::string*, Dot>> ins;
+    bool own = false;  // aliased batch: copy the strings (their map may change before commit)
+    std::vector<std::pair<std::string, Dot>> ins_own;
+
+    // dst's slots dr[0, m); sources: slots sr[sfirst[s], sfirst[s + 1]) for s in [s0, s1)
+    void plan(const SlotRef* dr, uint32_t m, const uint64_t* ok, const uint32_t* oa, const uint64_t* oc, uint32_t o,
+              uint32_t c, const SlotRef* sr, const uint32_t* sfirst, uint32_t s0, uint32_t s1) {
+        erase.clear();
+        upd.clear();
+        ins.clear();
+        ins_own.clear();
+        uint32_t i = 0, j = 0;
+        while (i < c || j < m) {
+            if (j < m && (i == c || dr[j].id < ok[o + i])) {
+                erase.push_back(dr[j].it);
+                ++j;
+            } else if (j < m && dr[j].id == ok[o + i]) {
+                const Dot nd{oa[o + i], oc[o + i]};
+                if (dr[j].dot != nd) upd.emplace_back(dr[j].it, nd);
+                ++i, ++j;
+            } else {  // a key the destination did not hold: its string is a source's
+                const uint64_t id = ok[o + i];
+                const std::string* name = nullptr;
+                for (uint32_t q = s0; q < s1 && !name; ++q) {
+                    const SlotRef* lo = sr + sfirst[q];
+                    const SlotRef* hi = sr + sfirst[q + 1];
+                    const SlotRef* f =
+                        std::lower_bound(lo, hi, id, [](const SlotRef& x, uint64_t v) { return x.id < v; });
+                    if (f != hi && f->id == id) name = &f->it->first;
+                }
+                if (!name) throw Error(CRDT_E_INVALID, "merge result holds a key no state of its document had");
+                if (own)
+                    ins_own.emplace_back(*name, Dot{oa[o + i], oc[o + i]});
+                else
+                    ins.emplace_back(name, Dot{oa[o + i], oc[o + i]});
+                ++i;
+            }
+        }
+    }
+    void commit(AWSet& dst) {
+        for (auto it : erase) dst.entries.erase(it);
+        for (auto& u : upd) u.first->second = u.second;
+        if (!ins.empty() || !ins_own.empty()) {
+            dst.entries.reserve(dst.entries.size() + ins.size() + ins_own.size());
+            for (auto& x : ins) dst.entries.emplace(*x.first, x.second);
+            for (auto& x : ins_own) dst.entries.emplace(std::move(x.first), x.second);
+        }
+    }
+};
+
+// Destinations must be distinct; true when some source is also a destination
+// of the batch, so that every plan must be made before any map changes.
+inline bool aliased(const std::vector<AWSet*>& dsts, const std::vector<const AWSet*>& srcs, const char* what) {
+    std::unordered_map<const AWSet*, int> seen;
+    seen.reserve(dsts.size());
+    for (auto* d : dsts)
+        if (!seen.emplace(d, 0).second) throw Error(CRDT_E_INVALID, std::string(what) + ": a destination appears twice");
+    for (auto* s : srcs)
+        if (seen.count(s)) return true;
+    return false;
+}
+
+// Per document: plan (read only) then commit (the destination maps change).
+// Unaliased batches do both per document on its thread; aliased ones make
+// every plan first (strings copied), then commit.
+struct DocPlan {
+    Plan a, b;  // b: the second direction of an exchange
+};
+
+template <typename PlanFn, typename CommitFn>
+void apply_docs(size_t n, bool alias, PlanFn&& plan_fn, CommitFn&& commit_fn) {
+    if (!alias) {
+        parallel_docs(n, [&](size_t lo, size_t hi) {
+            DocPlan p;
+            for (size_t d = lo; d < hi; ++d) {
+                plan_fn(d, p);
+                commit_fn(d, p);
+            }
+        });
+        return;
+    }
+    std::vector<DocPlan> plans(n);
     parallel_docs(n, [&](size_t lo, size_t hi) {
-        for (size_t d = lo; d < hi; ++d) b.intern(d, states_of(d));
+        for (size_t d = lo; d < hi; ++d) {
+            plans[d].a.own = plans[d].b.own = true;
+            plan_fn(d, plans[d]);
+        }
+    });
+    parallel_docs(n, [&](size_t lo, size_t hi) {
+        for (size_t d = lo; d < hi; ++d) commit_fn(d, plans[d]);
     });
 }
-
 }  // namespace detail
+
 
 namespace detail {
 struct GoPanic {};
@@ -458,43 +640,20 @@ size_t ragged_checks(int mode, size_t n_docs, F&& states_of, const char* what) {
 }
 }  // namespace detail
 
-// dsts[i].Merge(*srcs[i]) for every i, as one batched GPU join.
-inline void MergeBatch(const std::vector<AWSet*>& dsts, const std::vector<const AWSet*>& srcs,
-                       Engine& e = Engine::Default()) {
-    if (dsts.size() != srcs.size()) throw Error(CRDT_E_INVALID, "MergeBatch: length mismatch");
-    if (dsts.empty()) return;
-    detail::Batch b;
-    b.R = detail::ragged_checks(
-        CRDT_FOLD_AWSET, dsts.size(), [&](size_t d) { return std::vector<const AWSet*>{dsts[d], srcs[d]}; },
-        "MergeBatch");
-    detail::intern_all(b, dsts.size(), [&](size_t d) { return std::vector<const AWSet*>{dsts[d], srcs[d]}; });
-    std::vector<AWSet*> sv;
-    for (auto* s : srcs) sv.push_back(const_cast<AWSet*>(s));
-    detail::Packed pd = b.pack(dsts), ps = b.pack(sv);
-    crdt_awset_batch cd = b.view(pd), cs = b.view(ps);
-    std::vector<uint32_t> counts;
-    crdt_awset_out co;
-    detail::Packed po = detail::make_out(dsts.size(), b.R, pd.keys.size() + ps.keys.size(), counts, co);
-    check(crdt_awset_join_batch(e.ctx(), &cd, &cs, &co), "crdt_awset_join_batch");
-    std::vector<size_t> widths;
-    for (size_t i = 0; i < dsts.size(); ++i)
-        widths.push_back(std::max(dsts[i]->versionVector.size(), srcs[i]->versionVector.size()));
-    b.unpack(dsts, po, counts, widths);
-}
-
 namespace detail {
 // len(dst.versionVector) after the fold, replayed on the VVs alone: a delta
 // step that brings nothing (awset-delta_test.go:60) skips VersionVector.Merge.
 // A step merges iff Counter(src.Actor) == 0 (:53) or MakeDeltaMergeData finds
 // a changed entry or an effective tombstone (:79-105).
-inline size_t fold_width(int mode, const AWSet& dst, const std::vector<const AWSet*>& srcs) {
+inline size_t fold_width(int mode, const AWSet& dst, const AWSet* const* srcs, size_t ns) {
     size_t n = dst.versionVector.size();
     if (mode != CRDT_FOLD_DELTA) {
-        for (auto* s : srcs) n = std::max(n, s->versionVector.size());
+        for (size_t i = 0; i < ns; ++i) n = std::max(n, srcs[i]->versionVector.size());
         return n;
     }
     std::vector<uint64_t> V(dst.versionVector.begin(), dst.versionVector.end());
-    for (auto* s : srcs) {
+    for (size_t q = 0; q < ns; ++q) {
+        const AWSet* s = srcs[q];
         if ((s->actor < V.size() ? V[s->actor] : 0) != 0) {
             bool any = false;
             for (auto& kv : s->entries)
@@ -519,62 +678,222 @@ inline size_t fold_width(int mode, const AWSet& dst, const std::vector<const AWS
     return V.size();
 }
 
+// Lay out and pack a batch into the engine's page-locked SoA arrays.
+// Returns the destination batch; the sources' arrays are left in the
+// engine's kS_* staging.
+inline crdt_awset_batch pack(Batch& b, Engine& e, bool tombs) {
+    layout(b, tombs);
+    const size_t n = b.n_docs, ns = b.src.size(), R = b.R;
+    const size_t nd = b.dfirst[n], nse = b.sfirst[ns], nt = b.tfirst[ns];
+    uint32_t* doff = e.pinned<uint32_t>(kD_OFF, n + 1);
+    std::copy(b.dfirst.begin(), b.dfirst.end(), doff);
+    uint32_t* soff = e.pinned<uint32_t>(kS_OFF, ns + 1);
+    std::copy(b.sfirst.begin(), b.sfirst.end(), soff);
+    uint64_t* dk = e.pinned<uint64_t>(kD_KEY, nd);
+    uint32_t* da = e.pinned<uint32_t>(kD_ACT, nd);
+    uint64_t* dc = e.pinned<uint64_t>(kD_CTR, nd);
+    uint64_t* dv = e.pinned<uint64_t>(kD_VV, n * R);
+    uint64_t* sk = e.pinned<uint64_t>(kS_KEY, nse);
+    uint32_t* sa = e.pinned<uint32_t>(kS_ACT, nse);
+    uint64_t* sc = e.pinned<uint64_t>(kS_CTR, nse);
+    uint64_t* sv = e.pinned<uint64_t>(kS_VV, ns * R);
+    uint64_t *tk = nullptr, *tc = nullptr;
+    uint32_t* ta = nullptr;
+    if (tombs && nt) {
+        tk = e.pinned<uint64_t>(kS_TKEY, nt);
+        ta = e.pinned<uint32_t>(kS_TACT, nt);
+        tc = e.pinned<uint64_t>(kS_TCTR, nt);
+    }
+    std::vector<unsigned> rank_count(host_threads() + 1, 0);
+    parallel_docs(n, [&](size_t lo, size_t hi) {
+        DocPacker pk{b, dk, sk, tk, dc, sc, tc, da, sa, ta, {}, {}, {}, false};
+        for (size_t d = lo; d < hi; ++d) {
+            pk.doc(d);
+            const auto& v = b.dst[d]->versionVector;
+            for (size_t r = 0; r < R; ++r) dv[d * R + r] = r < v.size() ? v[r] : 0;
+            for (uint32_t q = b.src_beg[d]; q < b.src_beg[d + 1]; ++q) {
+                const auto& w = b.src[q]->versionVector;
+                for (size_t r = 0; r < R; ++r) sv[q * R + r] = r < w.size() ? w[r] : 0;
+            }
+        }
+    });
+    size_t ranks = 0;
+    for (auto x : b.rank_doc) ranks += x;
+    LastStats().rank_docs = ranks;
+    return crdt_awset_batch{(uint32_t)n, (uint32_t)R, doff, nullptr, dk, da, dc, dv};
+}
+
+inline crdt_awset_out out_arrays(Engine& e, int first_role, size_t n, size_t R, size_t slots) {
+    return crdt_awset_out{e.pinned<uint32_t>(first_role + 0, n + 1), e.pinned<uint32_t>(first_role + 1, n),
+                          e.pinned<uint64_t>(first_role + 2, slots), e.pinned<uint32_t>(first_role + 3, slots),
+                          e.pinned<uint64_t>(first_role + 4, slots), e.pinned<uint64_t>(first_role + 5, n * R)};
+}
+
+inline crdt_awset_batch src_view(const Batch& b, Engine& e) {
+    const size_t n = b.n_docs, R = b.R;
+    return crdt_awset_batch{(uint32_t)n,
+                            (uint32_t)R,
+                            e.pinned<uint32_t>(kS_OFF, n + 1),
+                            nullptr,
+                            e.pinned<uint64_t>(kS_KEY, 0),
+                            e.pinned<uint32_t>(kS_ACT, 0),
+                            e.pinned<uint64_t>(kS_CTR, 0),
+                            e.pinned<uint64_t>(kS_VV, 0)};
+}
+
+inline void set_vv(AWSet& dst, const uint64_t* vv, size_t width) { dst.versionVector.assign(vv, vv + width); }
+
+inline Batch join_batch(const std::vector<AWSet*>& dsts, const std::vector<const AWSet*>& srcs, const char* what) {
+    if (dsts.size() != srcs.size()) throw Error(CRDT_E_INVALID, std::string(what) + ": length mismatch");
+    Batch b;
+    b.n_docs = dsts.size();
+    b.R = ragged_checks(
+        CRDT_FOLD_AWSET, b.n_docs, [&](size_t d) { return std::vector<const AWSet*>{dsts[d], srcs[d]}; }, what);
+    b.dst = dsts;
+    b.src = srcs;
+    b.src_beg.resize(b.n_docs + 1);
+    for (size_t d = 0; d <= b.n_docs; ++d) b.src_beg[d] = (uint32_t)d;
+    return b;
+}
+}  // namespace detail
+
+// dsts[i].Merge(*srcs[i]) for every i, as one batched GPU join (dsts distinct).
+inline void MergeBatch(const std::vector<AWSet*>& dsts, const std::vector<const AWSet*>& srcs,
+                       Engine& e = Engine::Default()) {
+    using namespace detail;
+    if (dsts.empty() && srcs.empty()) return;
+    auto t0 = clk::now();
+    Batch b = join_batch(dsts, srcs, "MergeBatch");
+    const crdt_awset_batch cd = pack(b, e, false), cs = src_view(b, e);
+    const size_t n = b.n_docs, slots = (size_t)b.dfirst[n] + b.sfirst[n];
+    const crdt_awset_out co = out_arrays(e, kO_OFF, n, b.R, slots);
+    LastStats().pack_s = secs_since(t0);
+    t0 = clk::now();
+    check(crdt_awset_join_batch(e.ctx(), &cd, &cs, &co), "crdt_awset_join_batch");
+    LastStats().device_s = secs_since(t0);
+    t0 = clk::now();
+    apply_docs(
+        n, aliased(b.dst, b.src, "MergeBatch"),
+        [&](size_t d, DocPlan& p) {
+            p.a.plan(b.dref.data() + b.dfirst[d], b.dfirst[d + 1] - b.dfirst[d], co.keys, co.actors, co.counters,
+                     co.offsets[d], co.counts[d], b.sref.data(), b.sfirst.data(), (uint32_t)d, (uint32_t)d + 1);
+        },
+        [&](size_t d, DocPlan& p) {
+            const size_t w = std::max(b.dst[d]->versionVector.size(), b.src[d]->versionVector.size());
+            p.a.commit(*b.dst[d]);
+            set_vv(*b.dst[d], co.vv + d * b.R, w);
+        });
+    LastStats().apply_s = secs_since(t0);
+}
+
+// Anti-entropy both ways: for every i, as[i] <- bs[i] and bs[i] <- as[i],
+// the two merges of ONE snapshot (crdt_awset_exchange_batch; each equals
+// x := a.Clone(); x.Merge(b) resp. y := b.Clone(); y.Merge(a)), applied in
+// place to both maps.
+inline void ExchangeBatch(const std::vector<AWSet*>& as, const std::vector<AWSet*>& bs,
+                          Engine& e = Engine::Default()) {
+    using namespace detail;
+    if (as.empty() && bs.empty()) return;
+    auto t0 = clk::now();
+    Batch b = join_batch(as, std::vector<const AWSet*>(bs.begin(), bs.end()), "ExchangeBatch");
+    const crdt_awset_batch ca = pack(b, e, false), cb = src_view(b, e);
+    const size_t n = b.n_docs, slots = (size_t)b.dfirst[n] + b.sfirst[n];
+    const crdt_awset_out oab = out_arrays(e, kO_OFF, n, b.R, slots), oba = out_arrays(e, kP_OFF, n, b.R, slots);
+    LastStats().pack_s = secs_since(t0);
+    t0 = clk::now();
+    check(crdt_awset_exchange_batch(e.ctx(), &ca, &cb, &oab, &oba), "crdt_awset_exchange_batch");
+    LastStats().device_s = secs_since(t0);
+    t0 = clk::now();
+    {
+        std::vector<AWSet*> all(as);
+        all.insert(all.end(), bs.begin(), bs.end());
+        aliased(all, {}, "ExchangeBatch");  // every state distinct: no document reads another's map
+    }
+    apply_docs(
+        n, false,
+        [&](size_t d, DocPlan& p) {  // both plans read the untouched maps ...
+            p.a.plan(b.dref.data() + b.dfirst[d], b.dfirst[d + 1] - b.dfirst[d], oab.keys, oab.actors, oab.counters,
+                     oab.offsets[d], oab.counts[d], b.sref.data(), b.sfirst.data(), (uint32_t)d, (uint32_t)d + 1);
+            p.b.plan(b.sref.data() + b.sfirst[d], b.sfirst[d + 1] - b.sfirst[d], oba.keys, oba.actors, oba.counters,
+                     oba.offsets[d], oba.counts[d], b.dref.data(), b.dfirst.data(), (uint32_t)d, (uint32_t)d + 1);
+        },
+        [&](size_t d, DocPlan& p) {  // ... then each map changes
+            const size_t w = std::max(as[d]->versionVector.size(), bs[d]->versionVector.size());
+            p.a.commit(*as[d]);
+            p.b.commit(*bs[d]);
+            set_vv(*as[d], oab.vv + d * b.R, w);
+            set_vv(*bs[d], oba.vv + d * b.R, w);
+        });
+    LastStats().apply_s = secs_since(t0);
+}
+
+namespace detail {
 inline void fold(int mode, const std::vector<AWSet*>& dsts, const std::vector<std::vector<const AWSet*>>& srcs,
                  Engine& e) {
     if (dsts.size() != srcs.size()) throw Error(CRDT_E_INVALID, "fold: length mismatch");
     if (dsts.empty()) return;
+    auto t0 = clk::now();
     Batch b;
+    b.n_docs = dsts.size();
     b.R = ragged_checks(
-        mode, dsts.size(),
+        mode, b.n_docs,
         [&](size_t d) {
             std::vector<const AWSet*> v{dsts[d]};
             v.insert(v.end(), srcs[d].begin(), srcs[d].end());
             return v;
         },
         mode == CRDT_FOLD_DELTA ? "DeltaMergeBatch" : "FoldBatch");
-    intern_all(b, dsts.size(), [&](size_t d) {
-        std::vector<const AWSet*> v{dsts[d]};
-        v.insert(v.end(), srcs[d].begin(), srcs[d].end());
-        return v;
-    });
-    Packed pd = b.pack(dsts);
-    std::vector<uint32_t> doc_srcs{0}, src_actor, entry_off{0}, tomb_off{0};
-    std::vector<uint64_t> vv, keys, counters, tkeys, tcounters;
-    std::vector<uint32_t> actors, tactors;
-    for (size_t d = 0; d < srcs.size(); ++d) {
-        for (auto* s : srcs[d]) {
-            src_actor.push_back(s->actor);
-            for (size_t r = 0; r < b.R; ++r) vv.push_back(r < s->versionVector.size() ? s->versionVector[r] : 0);
-            const size_t o = keys.size(), m = s->entries.size();
-            keys.resize(o + m);
-            actors.resize(o + m);
-            counters.resize(o + m);
-            b.put_entries(d, s->entries, keys.data() + o, actors.data() + o, counters.data() + o);
-            entry_off.push_back((uint32_t)keys.size());
-            if (auto* del = s->deleted_map()) {
-                const size_t t = tkeys.size(), x = del->size();
-                tkeys.resize(t + x);
-                tactors.resize(t + x);
-                tcounters.resize(t + x);
-                b.put_entries(d, *del, tkeys.data() + t, tactors.data() + t, tcounters.data() + t);
-            }
-            tomb_off.push_back((uint32_t)tkeys.size());
-        }
-        doc_srcs.push_back((uint32_t)src_actor.size());
+    b.dst = dsts;
+    for (auto& l : srcs) {
+        b.src.insert(b.src.end(), l.begin(), l.end());
+        b.src_beg.push_back((uint32_t)b.src.size());
     }
-    crdt_awset_batch cd = b.view(pd);
-    const bool tombs = !tkeys.empty();  // no tombstones at all: tomb_off = NULL
-    crdt_src_batch cs{(uint32_t)dsts.size(), (uint32_t)b.R, doc_srcs.data(), data_or_null(src_actor),
-                      data_or_null(vv), entry_off.data(), data_or_null(keys), data_or_null(actors),
-                      data_or_null(counters), tombs ? tomb_off.data() : nullptr, data_or_null(tkeys),
-                      data_or_null(tactors), data_or_null(tcounters)};
-    std::vector<uint32_t> counts;
-    crdt_awset_out co;
-    Packed po = make_out(dsts.size(), b.R, pd.keys.size() + keys.size(), counts, co);
+    const bool tomb_mode = mode == CRDT_FOLD_DELTA;
+    const crdt_awset_batch cd = pack(b, e, tomb_mode);
+    const size_t n = b.n_docs, ns = b.src.size(), R = b.R;
+    uint32_t* doc_srcs = e.pinned<uint32_t>(kS_DOC, n + 1);
+    std::copy(b.src_beg.begin(), b.src_beg.end(), doc_srcs);
+    uint32_t* sact = e.pinned<uint32_t>(kS_SACT, ns);
+    for (size_t q = 0; q < ns; ++q) sact[q] = b.src[q]->actor;
+    const bool tombs = tomb_mode && b.tfirst[ns] > 0;  // no tombstones at all: tomb_off = NULL
+    uint32_t* toff = nullptr;
+    if (tombs) {
+        toff = e.pinned<uint32_t>(kS_TOFF, ns + 1);
+        std::copy(b.tfirst.begin(), b.tfirst.end(), toff);
+    }
+    const crdt_src_batch cs{(uint32_t)n,
+                            (uint32_t)R,
+                            doc_srcs,
+                            sact,
+                            e.pinned<uint64_t>(kS_VV, 0),
+                            e.pinned<uint32_t>(kS_OFF, 0),
+                            e.pinned<uint64_t>(kS_KEY, 0),
+                            e.pinned<uint32_t>(kS_ACT, 0),
+                            e.pinned<uint64_t>(kS_CTR, 0),
+                            toff,
+                            tombs ? e.pinned<uint64_t>(kS_TKEY, 0) : nullptr,
+                            tombs ? e.pinned<uint32_t>(kS_TACT, 0) : nullptr,
+                            tombs ? e.pinned<uint64_t>(kS_TCTR, 0) : nullptr};
+    const size_t slots = (size_t)b.dfirst[n] + b.sfirst[ns];
+    const crdt_awset_out co = out_arrays(e, kO_OFF, n, R, slots);
+    LastStats().pack_s = secs_since(t0);
+    t0 = clk::now();
     check(crdt_awset_fold_batch(e.ctx(), mode, &cd, &cs, &co), "crdt_awset_fold_batch");
-    std::vector<size_t> widths;
-    for (size_t i = 0; i < dsts.size(); ++i) widths.push_back(fold_width(mode, *dsts[i], srcs[i]));
-    b.unpack(dsts, po, counts, widths);
+    LastStats().device_s = secs_since(t0);
+    t0 = clk::now();
+    apply_docs(
+        n, aliased(b.dst, b.src, "fold"),
+        [&](size_t d, DocPlan& p) {
+            p.a.plan(b.dref.data() + b.dfirst[d], b.dfirst[d + 1] - b.dfirst[d], co.keys, co.actors, co.counters,
+                     co.offsets[d], co.counts[d], b.sref.data(), b.sfirst.data(), b.src_beg[d], b.src_beg[d + 1]);
+        },
+        [&](size_t d, DocPlan& p) {
+            const uint32_t s0 = b.src_beg[d], s1 = b.src_beg[d + 1];
+            const size_t w = fold_width(mode, *b.dst[d], b.src.data() + s0, s1 - s0);
+            p.a.commit(*b.dst[d]);
+            set_vv(*b.dst[d], co.vv + d * R, w);
+        });
+    LastStats().apply_s = secs_since(t0);
 }
 }  // namespace detail
 

@@ -352,7 +352,12 @@ int crdt_comm_unique_id(uint8_t* id /* [CRDT_COMM_ID_BYTES] */);
 int crdt_comm_init(crdt_ctx* ctx, int n_ranks, int rank, const uint8_t* id);
 int crdt_context_allreduce_async(crdt_ctx* ctx, uint64_t* vv_R, uint32_t R, void* stream);
 
-/* ---- host buffers, synchronous: copies in, runs, copies out ------------- */
+/* ---- host buffers, synchronous: copies in, runs, copies out -------------
+ * Host arrays from crdt_host_alloc (page-locked) cross PCIe by DMA at full
+ * link rate; pageable arrays work too, staged by the HIP runtime.  A caller
+ * packing many batches keeps its page-locked arrays and reuses them. */
+int crdt_host_alloc(size_t bytes, void** out);
+void crdt_host_free(void* p);
 int crdt_awset_join_batch(crdt_ctx* ctx, const crdt_awset_batch* dst, const crdt_awset_batch* src,
                           const crdt_awset_out* out);
 int crdt_awset_exchange_batch(crdt_ctx* ctx, const crdt_awset_batch* a, const crdt_awset_batch* b,

@@ -236,6 +236,47 @@ static void TestBatches() {
     expect(d, {{"p", {1, 1}}, {"q", {2, 1}}}, {0, 2, 1});
 }
 
+// ExchangeBatch = the two merges of one snapshot, applied in place; an
+// aliased MergeBatch (a <- b and b <- a in one batch) reads the snapshot too.
+static void TestExchangeAndAliasing() {
+    std::vector<AWSet> as, bs, xs, ys;
+    for (int i = 0; i < 300; ++i) {
+        AWSet a(0, {0, 0}), b(1, {0, 0});
+        for (int j = 0; j < i % 11; ++j) a.Add({"k" + std::to_string(j)});
+        b.Merge(a);
+        for (int j = 0; j < i % 7; ++j) b.Add({"k" + std::to_string(2 * j + 1)});
+        if (i % 3 == 0) a.Del({"k0", "k2"});
+        if (i % 4 == 0) b.Del({"k1"});
+        AWSet x = a, y = b;
+        x.Merge(b);
+        y.Merge(a);
+        as.push_back(a), bs.push_back(b), xs.push_back(x), ys.push_back(y);
+    }
+    std::vector<AWSet*> pa, pb;
+    for (size_t i = 0; i < as.size(); ++i) pa.push_back(&as[i]), pb.push_back(&bs[i]);
+    ExchangeBatch(pa, pb);
+    for (size_t i = 0; i < as.size(); ++i) {
+        CHECK(as[i].entries == xs[i].entries && as[i].versionVector == xs[i].versionVector);
+        CHECK(bs[i].entries == ys[i].entries && bs[i].versionVector == ys[i].versionVector);
+    }
+    AWSet a(0, {0, 0}), b(1, {0, 0});
+    a.Add({"x", "y"});
+    b.Add({"y", "z"});
+    AWSet x = a, y = b;
+    x.Merge(b);
+    y.Merge(a);
+    MergeBatch({&a, &b}, {&b, &a});
+    CHECK(a.entries == x.entries && a.versionVector == x.versionVector);
+    CHECK(b.entries == y.entries && b.versionVector == y.versionVector);
+    bool threw = false;
+    try {
+        MergeBatch({&a, &a}, {&b, &b});
+    } catch (const Error& e) {
+        threw = e.code == CRDT_E_INVALID;
+    }
+    CHECK(threw);  // a destination twice
+}
+
 int main() {
     TestAWSetXXX();
     TestAWSet();
@@ -246,6 +287,7 @@ int main() {
     TestPanicsBecomeErrors();
     TestRaggedVectors();
     TestBatches();
+    TestExchangeAndAliasing();
     std::printf("%s: %d failure(s)\n", failures ? "FAILED" : "ok", failures);
     return failures ? 1 : 0;
 }

@@ -14,9 +14,13 @@ BIN = os.path.join(ROOT, "go-crdt-playground_amd", "host", "build", "test_scenar
 
 
 @pytest.mark.gpu
-def test_cpp_scenarios_on_gpu():
+@pytest.mark.parametrize("rank_ids", ["0", "1"])
+def test_cpp_scenarios_on_gpu(rank_ids):
+    """rank_ids=1: every document takes the mirror's hash-collision fallback
+    (ids = the keys' ranks in string order) instead of 64-bit hash ids."""
     assert os.path.exists(BIN), "build() first"
-    r = subprocess.run([BIN], capture_output=True, text=True, timeout=100)
+    env = dict(os.environ, CRDT_HOST_RANK_IDS=rank_ids)
+    r = subprocess.run([BIN], capture_output=True, text=True, timeout=100, env=env)
     print(r.stdout, r.stderr)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "ok: 0 failure(s)" in r.stdout
