@@ -75,7 +75,7 @@ def box_probe(eng, dev, nbytes=2 << 30, reps=10):
         return max(v for k, v in variants.items() if k.startswith(prefix))
 
     return {"bytes": nbytes, "reps": reps, "read_gbs": best("read"), "write_gbs": best("write"),
-            "copy_gbs": best("copy"), "variants": variants}
+            "copy_gbs": best("copy"), "sclk_mhz": eng.clock_probe(), "variants": variants}
 
 
 def _np_copy(t, n, dt):
@@ -473,6 +473,7 @@ def _box_fields(roof, box):
         roof["box_write_gbs"] = box["write_gbs"]
         roof["box_copy_gbs"] = box["copy_gbs"]
         roof["frac_vs_box"] = a / box["copy_gbs"] if box["copy_gbs"] else None
+        roof["box_sclk_mhz"] = box.get("sclk_mhz")
 
 
 def run_config(config, n, args, ctx, steps, warmup, repeats, cpu, box=None):
@@ -717,7 +718,8 @@ def main():
     if box:
         result["box_probe"] = dict(box, what="crdt_bw_probe on this box before timing: streaming read (16 B/lane), "
                                              "write and copy (read+write bytes), best of nt/plain stores and 8/16/32 "
-                                             "workgroups per CU; roofline.frac_vs_box = achieved / copy_gbs")
+                                             "workgroups per CU; roofline.frac_vs_box = achieved / copy_gbs; sclk_mhz: "
+                                             "shader clock under an all-CU integer load (crdt_clock_probe)")
     if legs:
         result["legs"] = {}
         for c in legs:

@@ -149,6 +149,7 @@ def _load():
                                          P(ctypes.c_double)]),
         "crdt_host_alloc": (ctypes.c_int, [ctypes.c_size_t, P(_vp)]),
         "crdt_host_free": (None, [_vp]),
+        "crdt_clock_probe": (ctypes.c_int, [_vp, P(ctypes.c_double)]),
         "crdt_validate_batch": (ctypes.c_int, [P(CAWSetBatch)]),
         "crdt_validate_src_batch": (ctypes.c_int, [P(CSrcBatch)]),
         "crdt_validate_tomb_batch": (ctypes.c_int, [P(CTombBatch), _u32]),

@@ -61,6 +61,12 @@ class Engine:
     def sync(self, stream=None):
         check(self._lib.crdt_ctx_sync(self._ctx, _stream(stream)), "crdt_ctx_sync")
 
+    def clock_probe(self) -> float:
+        """Shader clock in MHz under an all-CU integer load (crdt_clock_probe)."""
+        g = ctypes.c_double()
+        check(self._lib.crdt_clock_probe(self._ctx, ctypes.byref(g)), "crdt_clock_probe")
+        return g.value
+
     def bw_probe(self, kind: int, a, b, nbytes: int, reps: int = 10) -> float:
         """GB/s of a streaming read / write / copy over device buffers a, b (crdt_bw_probe)."""
         g = ctypes.c_double()

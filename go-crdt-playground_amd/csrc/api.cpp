@@ -51,6 +51,7 @@ hipError_t launch_gen_replicas(uint64_t seed, uint32_t n_docs, uint32_t P, uint3
 hipError_t launch_gen_zipf(uint64_t seed, uint32_t n_docs, const uint32_t* offsets, const OutView& A,
                            const OutView& B, hipStream_t stream);
 uint32_t host_zipf_doc_size(uint64_t seed, uint32_t d);
+hipError_t launch_clock_probe(uint64_t* out, uint32_t n_cu, hipStream_t stream);
 hipError_t launch_probe(int kind, const void* a, void* b, size_t n16, uint32_t n_cu, uint32_t blocks_per_cu,
                         hipStream_t stream);
 }  // namespace crdt
@@ -633,6 +634,27 @@ int crdt_host_alloc(size_t bytes, void** out) {
 
 void crdt_host_free(void* p) {
     if (p) (void)hipHostFree(p);
+}
+
+int crdt_clock_probe(crdt_ctx* ctx, double* mhz) {
+    if (!ctx || !mhz) return CRDT_E_INVALID;
+    int rc = set_device(ctx);
+    if (rc != CRDT_OK) return rc;
+    hipStream_t s = ctx->stream;
+    bool cap = false;
+    if ((rc = enter(ctx, s, cap)) != CRDT_OK) return rc;
+    if (cap) return CRDT_E_INVALID;
+    int wall_khz = 0;
+    if (hipDeviceGetAttribute(&wall_khz, hipDeviceAttributeWallClockRate, ctx->device) != hipSuccess || wall_khz <= 0)
+        return CRDT_E_HIP;
+    uint64_t* dev = ctx->parts.as<uint64_t>();  // 3 words of the context-summary partials, free between calls
+    uint64_t host[2] = {0, 0};
+    rc = hip_err(launch_clock_probe(dev, (uint32_t)ctx->n_cu, s));  // warm-up: clocks ramp up
+    if (rc == CRDT_OK) rc = hip_err(launch_clock_probe(dev, (uint32_t)ctx->n_cu, s));
+    if (rc == CRDT_OK) rc = hip_err(hipMemcpyAsync(host, dev, sizeof(host), hipMemcpyDeviceToHost, s));
+    if (rc == CRDT_OK) rc = hip_err(hipStreamSynchronize(s));
+    if (rc == CRDT_OK) *mhz = host[1] ? (double)host[0] / ((double)host[1] / ((double)wall_khz * 1e3)) / 1e6 : 0.0;
+    return leave(ctx, s, cap, rc);
 }
 
 /* ---------------- validation (host) ---------------- */

@@ -108,8 +108,103 @@ struct Emit {
 // The current dot is the last entry's, whatever the presence, so it is one
 // segmented scan; with the gap folded in, each tuple is again constant or
 // identity, and the final presence is the last constant: a second scan.
+// Wave reductions over u32 lanes (DPP row shifts and broadcasts; lanes with no
+// source take the identity); every lane gets the result.
+template <bool MAX>
+__device__ __forceinline__ uint32_t wave_minmax(uint32_t x) {
+    const uint32_t id = MAX ? 0u : ~0u;
+    auto op = [](uint32_t a, uint32_t b) { return MAX ? max(a, b) : min(a, b); };
+    x = op(x, dpp<0x111>(id, x));       // row_shr:1
+    x = op(x, dpp<0x112>(id, x));       // row_shr:2
+    x = op(x, dpp<0x114>(id, x));       // row_shr:4
+    x = op(x, dpp<0x118>(id, x));       // row_shr:8
+    x = op(x, dpp<0x142, 0xA>(id, x));  // row_bcast:15
+    x = op(x, dpp<0x143, 0xC>(id, x));  // row_bcast:31
+    return (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
+}
+
+// Inclusive prefix sum over lanes (DPP).
+__device__ __forceinline__ uint32_t wave_incl_sum(uint32_t x) {
+    x += dpp<0x111>(0u, x);
+    x += dpp<0x112>(0u, x);
+    x += dpp<0x114>(0u, x);
+    x += dpp<0x118>(0u, x);
+    x += dpp<0x142, 0xA>(0u, x);
+    x += dpp<0x143, 0xC>(0u, x);
+    return x;
+}
+
+// Counting sort of the kept (key, tag) pairs, used instead of the bitonic
+// network when the document's kept keys span fewer than 256 ids and every
+// tag's step field (tag >> 8) is below 32 -- the common case for keys
+// interned per document (host/crdt.hpp: ranks, or the generator's dense ids).
+// ev[s] = the set of step fields present at key slot s (keys of one document
+// are distinct per state, so a (slot, step field) pair occurs once); a pair's
+// sorted position is the exclusive prefix over slots of popc(ev) plus its rank
+// in its slot's mask, which is (key, tag) order.  Scratch aliases tk, stag and
+// smark, all dead once k / t are in registers.  Returns false (nothing
+// changed) when the document does not qualify.
+template <int EPL, class Smem>
+__device__ __forceinline__ bool dense_sort(Smem& m, uint64_t (&k)[EPL], uint32_t (&t)[EPL], uint32_t n,
+                                           uint32_t lane) {
+    if (n == 0) return true;
+    const uint64_t b = readlane64(k[0], 0);  // element 0 is valid
+    bool bad = false;
+    uint32_t lo = ~0u, hi = 0u;
+#pragma unroll
+    for (int q = 0; q < EPL; ++q) {
+        const bool valid = lane * EPL + q < n;
+        const uint64_t d = k[q] - b + 0x80000000ull;  // biased: u32 order = signed offset order
+        bad |= valid && ((d >> 32) != 0 || (t[q] >> 8) >= 32u);
+        lo = valid ? min(lo, (uint32_t)d) : lo;
+        hi = valid ? max(hi, (uint32_t)d) : hi;
+    }
+    if (ballot(bad)) return false;
+    lo = wave_minmax<false>(lo);
+    hi = wave_minmax<true>(hi);
+    if (hi - lo >= 256u) return false;
+    uint32_t* ev = reinterpret_cast<uint32_t*>(m.tk);
+    uint16_t* base = reinterpret_cast<uint16_t*>(m.tk + 128);
+    reinterpret_cast<uint4*>(ev)[lane] = make_uint4(0u, 0u, 0u, 0u);
+    wave_sync();
+    uint32_t sl[EPL], hb[EPL];
+#pragma unroll
+    for (int q = 0; q < EPL; ++q) {
+        sl[q] = (uint32_t)(k[q] - b + 0x80000000ull) - lo;
+        hb[q] = t[q] >> 8;
+        if (lane * EPL + q < n) atomicOr(&ev[sl[q] & 255u], 1u << (hb[q] & 31u));
+    }
+    wave_sync();
+    const uint4 e4 = reinterpret_cast<const uint4*>(ev)[lane];
+    const uint32_t c0 = __popc(e4.x), c1 = __popc(e4.y), c2 = __popc(e4.z), c3 = __popc(e4.w);
+    const uint32_t tot = c0 + c1 + c2 + c3;
+    const uint32_t pre = wave_incl_sum(tot) - tot;
+    reinterpret_cast<ushort4*>(base)[lane] =
+        make_ushort4((uint16_t)pre, (uint16_t)(pre + c0), (uint16_t)(pre + c0 + c1), (uint16_t)(pre + c0 + c1 + c2));
+    wave_sync();
+#pragma unroll
+    for (int q = 0; q < EPL; ++q) {
+        if (lane * EPL + q < n) {
+            const uint32_t s = sl[q] & 255u;
+            const uint32_t pos = base[s] + __popc(ev[s] & ((1u << (hb[q] & 31u)) - 1u));
+            m.stag[pos] = (uint16_t)t[q];
+            m.smark[pos] = (uint8_t)s;
+        }
+    }
+    wave_sync();
+    const uint64_t kb = b - 0x80000000ull + lo;
+#pragma unroll
+    for (int q = 0; q < EPL; ++q) {
+        const uint32_t i = lane * EPL + q;
+        const bool valid = i < n;
+        t[q] = valid ? (uint32_t)m.stag[i] : kPadTag;
+        k[q] = valid ? kb + m.smark[i] : ~0ull;
+    }
+    return true;
+}
+
 template <int EPL, bool DELTA, class Smem>
-__device__ __forceinline__ uint32_t sort_resolve(const Smem& m, uint32_t Kc, uint32_t ms, uint32_t R,
+__device__ __forceinline__ uint32_t sort_resolve(Smem& m, uint32_t Kc, uint32_t ms, uint32_t R,
                                                  uint64_t full_mask, uint32_t lane, uint64_t lt, Emit& e,
                                                  uint32_t& err STAMP_PARAM) {
     uint64_t k[EPL];
@@ -120,7 +215,7 @@ __device__ __forceinline__ uint32_t sort_resolve(const Smem& m, uint32_t Kc, uin
         k[q] = i < Kc ? m.tk[i] : ~0ull;
         t[q] = i < Kc ? (uint32_t)m.stag[i] : kPadTag;
     }
-    wave_sort_pairs<EPL>(k, t, Kc, lane);
+    if (!dense_sort<EPL>(m, k, t, Kc, lane)) wave_sort_pairs<EPL>(k, t, Kc, lane);
     STAMP(7)
     // the element after each one (the next lane's first for the last slot)
     const uint64_t k_nl = from_next_lane64(~0ull, k[0]);

@@ -57,6 +57,34 @@ __global__ __launch_bounds__(256) void probe_copy_kernel(const u32x4* __restrict
     for (; i < n; i += stride) put16<NT>(a[i], b + i);
 }
 
+// Shader clock under load: every CU runs dependent VALU chains; wave 0 of
+// block 0 reads the shader-cycle counter (s_memtime) and the fixed-rate
+// wall clock (s_memrealtime) around its loop.  out[0] = cycles, out[1] =
+// wall ticks.  Issue-bound kernels scale with this clock, streaming ones do
+// not -- boxes of one pool differ in both.
+__global__ __launch_bounds__(256) void probe_clock_kernel(uint64_t* out, uint32_t iters, uint32_t seed) {
+    uint32_t x = threadIdx.x ^ seed, y = x * 7u + 1u;
+    const uint64_t t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
+    for (uint32_t i = 0; i < iters; ++i) {
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+            x = x * 0x9E3779B1u + y;
+            y = y ^ (x >> 7);
+        }
+    }
+    const uint64_t t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        out[0] = t1 - t0;
+        out[1] = r1 - r0;
+    }
+    if (x == 0x12345678u && y == 0x9ABCDEF0u) out[2] = x;  // keeps the chain live
+}
+
+hipError_t launch_clock_probe(uint64_t* out, uint32_t n_cu, hipStream_t stream) {
+    hipLaunchKernelGGL(probe_clock_kernel, dim3(n_cu * 8u), dim3(256), 0, stream, out, 20000u, 0x5EEDu);
+    return hipGetLastError();
+}
+
 // kind (crdtgpu.h CRDT_PROBE_*): 0 read a, 1 write b (nt), 2 copy a -> b (nt),
 // 3 write b (plain stores), 4 copy (plain stores); n16 = 16-byte words;
 // blocks_per_cu workgroups of 256 threads per CU.

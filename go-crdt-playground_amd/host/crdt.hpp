@@ -157,10 +157,17 @@ class Engine {
     T* pinned(int role, size_t n) {
         return static_cast<T*>(pin_[role].get(n * sizeof(T)));
     }
+    // host arrays of map iterators per slot (0: destinations, 1: sources),
+    // grown on demand and reused: no per-call allocation or first touch
+    Entries::iterator* iters(int role, size_t n) {
+        if (its_[role].size() < n) its_[role].resize(n + n / 8);
+        return its_[role].data();
+    }
 
    private:
     crdt_ctx* ctx_ = nullptr;
     detail::PinnedBuf pin_[detail::kPinSlots];
+    std::vector<Entries::iterator> its_[2];
 };
 
 class AWSetDelta;
@@ -311,8 +318,9 @@ inline bool force_rank_ids() {
     return f;
 }
 
-// One packed slot: key id, the dot, and the map element it came from (its
-// key string; for a destination, the element the result updates in place).
+// One packed slot while a state is sorted: key id, the dot, and the map
+// element it came from (its key string; for a destination, the element the
+// result updates in place).
 struct SlotRef {
     uint64_t id;
     Dot dot;
@@ -321,7 +329,9 @@ struct SlotRef {
 
 // The states of a batch: role 0 = destinations (one per document), role 1 =
 // the sources (one per document for a join, any number for a fold); each
-// state's slots are contiguous, sorted by id, at first[role][state].
+// state's slots are contiguous and sorted by id at dfirst[state] /
+// sfirst[state] of the page-locked SoA arrays (dk/da/dc, sk/sa/sc) and of the
+// element iterators (dit, sit: the Engine's reusable host arrays).
 struct Batch {
     size_t R = 1;
     size_t n_docs = 0;
@@ -330,59 +340,97 @@ struct Batch {
     std::vector<uint32_t> src_beg{0};          // doc d's sources: [src_beg[d], src_beg[d+1])
     std::vector<uint32_t> dfirst, sfirst;      // per state: first slot (prefix of entry counts)
     std::vector<uint32_t> tfirst;              // per source: first tombstone slot
-    std::vector<SlotRef> dref, sref;           // per slot (host side of the SoA)
     std::vector<uint8_t> rank_doc;             // 1: ids of doc d are ranks (hash collision)
+    uint64_t *dk = nullptr, *dc = nullptr, *sk = nullptr, *sc = nullptr;
+    uint32_t *da = nullptr, *sa = nullptr;
+    Entries::iterator *dit = nullptr, *sit = nullptr;
 };
 
 // Fill doc d's slots: ids (hash, or ranks after a collision), sorted per
-// state, written to the page-locked SoA arrays and to the SlotRef arrays.
+// state, written to the page-locked SoA arrays and to the iterator arrays.
 struct DocPacker {
     Batch& b;
-    uint64_t *dk, *sk, *tk, *dc, *sc, *tc;
-    uint32_t *da, *sa, *ta;
+    uint64_t* tk;
+    uint64_t* tc;
+    uint32_t* ta;
     std::vector<std::pair<uint64_t, const std::string*>> names;  // thread-local scratch
     std::vector<const std::string*> sorted;                      // rank fallback scratch
     std::vector<SlotRef> tmp;
-
-    bool collect = false;  // hash pass: note (id, key) of every slot for the exact check
+    bool clash = false;
 
     template <typename IdOf>
-    void put_state(const Entries& m, uint32_t first, uint64_t* k, uint32_t* a, uint64_t* c, SlotRef* ref, IdOf&& id_of) {
+    void put_state(const Entries& m, uint32_t first, uint64_t* k, uint32_t* a, uint64_t* c, Entries::iterator* its,
+                   IdOf&& id_of) {
         tmp.clear();
-        for (auto it = const_cast<Entries&>(m).begin(); it != m.end(); ++it) tmp.push_back(SlotRef{id_of(it->first), it->second, it});
+        for (auto it = const_cast<Entries&>(m).begin(); it != m.end(); ++it)
+            tmp.push_back(SlotRef{id_of(it->first), it->second, it});
         std::sort(tmp.begin(), tmp.end(), [](const SlotRef& x, const SlotRef& y) { return x.id < y.id; });
         for (size_t i = 0; i < tmp.size(); ++i) {
             k[first + i] = tmp[i].id;
             a[first + i] = tmp[i].dot.actor;
             c[first + i] = tmp[i].dot.counter;
-            if (ref) ref[first + i] = tmp[i];
-            if (collect) names.emplace_back(tmp[i].id, &tmp[i].it->first);
+            if (its) its[first + i] = tmp[i].it;
+            // two keys of one state with one id: a collision (keys of a map are distinct)
+            if (i && tmp[i].id == tmp[i - 1].id) clash = true;
         }
     }
     template <typename IdOf>
     void put_doc(size_t d, IdOf&& id_of) {
-        put_state(b.dst[d]->entries, b.dfirst[d], dk, da, dc, b.dref.data(), id_of);
+        put_state(b.dst[d]->entries, b.dfirst[d], b.dk, b.da, b.dc, b.dit, id_of);
         for (uint32_t s = b.src_beg[d]; s < b.src_beg[d + 1]; ++s) {
-            put_state(b.src[s]->entries, b.sfirst[s], sk, sa, sc, b.sref.data(), id_of);
+            put_state(b.src[s]->entries, b.sfirst[s], b.sk, b.sa, b.sc, b.sit, id_of);
             if (tk)
                 if (auto* del = b.src[s]->deleted_map()) put_state(*del, b.tfirst[s], tk, ta, tc, nullptr, id_of);
         }
     }
-    void doc(size_t d) {
+    // Across states: equal ids must be equal strings.  Two states (a join): a
+    // merge of the two sorted id runs; more (a fold, or tombstones): one sort.
+    bool cross_clash(size_t d) {
+        const uint32_t s0 = b.src_beg[d], s1 = b.src_beg[d + 1];
+        const bool has_tombs = tk && b.tfirst[s1] > b.tfirst[s0];
+        if (s1 - s0 == 1 && !has_tombs) {
+            const uint64_t* x = b.dk + b.dfirst[d];
+            const uint64_t* y = b.sk + b.sfirst[s0];
+            const uint32_t nx = b.dfirst[d + 1] - b.dfirst[d], ny = b.sfirst[s0 + 1] - b.sfirst[s0];
+            for (uint32_t i = 0, j = 0; i < nx && j < ny;) {
+                if (x[i] < y[j]) {
+                    ++i;
+                } else if (y[j] < x[i]) {
+                    ++j;
+                } else {
+                    if (b.dit[b.dfirst[d] + i]->first != b.sit[b.sfirst[s0] + j]->first) return true;
+                    ++i, ++j;
+                }
+            }
+            return false;
+        }
         names.clear();
-        collect = true;
-        put_doc(d, [](const std::string& k) { return key_hash(k); });
-        collect = false;
-        // exact check: equal ids must be equal strings, over every state of the doc
+        for (uint32_t i = b.dfirst[d]; i < b.dfirst[d + 1]; ++i) names.emplace_back(b.dk[i], &b.dit[i]->first);
+        for (uint32_t i = b.sfirst[s0]; i < b.sfirst[s1]; ++i) names.emplace_back(b.sk[i], &b.sit[i]->first);
+        if (has_tombs)
+            for (uint32_t s = s0; s < s1; ++s)
+                if (auto* del = b.src[s]->deleted_map())
+                    for (auto& kv : *del) names.emplace_back(key_hash(kv.first), &kv.first);
         std::sort(names.begin(), names.end(), [](const auto& x, const auto& y) { return x.first < y.first; });
-        bool clash = force_rank_ids();
-        for (size_t i = 1; i < names.size() && !clash; ++i)
-            clash = names[i].first == names[i - 1].first && *names[i].second != *names[i - 1].second;
-        if (!clash) return;
+        for (size_t i = 1; i < names.size(); ++i)
+            if (names[i].first == names[i - 1].first && *names[i].second != *names[i - 1].second) return true;
+        return false;
+    }
+    void doc(size_t d) {
+        clash = false;
+        put_doc(d, [](const std::string& k) { return key_hash(k); });
+        if (!clash && !force_rank_ids() && !cross_clash(d)) return;
         // rank ids: the key's rank in string order over the doc's states
         b.rank_doc[d] = 1;
         sorted.clear();
-        for (auto& x : names) sorted.push_back(x.second);
+        auto add = [&](const Entries& m) {
+            for (auto& kv : m) sorted.push_back(&kv.first);
+        };
+        add(b.dst[d]->entries);
+        for (uint32_t s = b.src_beg[d]; s < b.src_beg[d + 1]; ++s) {
+            add(b.src[s]->entries);
+            if (auto* del = b.src[s]->deleted_map()) add(*del);
+        }
         auto lt = [](const std::string* x, const std::string* y) { return *x < *y; };
         std::sort(sorted.begin(), sorted.end(), lt);
         sorted.erase(std::unique(sorted.begin(), sorted.end(), [](auto* x, auto* y) { return *x == *y; }), sorted.end());
@@ -405,8 +453,6 @@ inline void layout(Batch& b, bool tombs) {
         b.tfirst[s + 1] = b.tfirst[s] + (uint32_t)(del ? del->size() : 0);
     }
     if ((uint64_t)b.dfirst[b.n_docs] + b.sfirst[ns] >= (1ull << 32)) throw Error(CRDT_E_INVALID, "batch too large");
-    b.dref.resize(b.dfirst[b.n_docs]);
-    b.sref.resize(b.sfirst[ns]);
     b.rank_doc.assign(b.n_docs, 0);
 }
 
@@ -423,31 +469,32 @@ struct Plan {
     bool own = false;  // aliased batch: copy the strings (their map may change before commit)
     std::vector<std::pair<std::string, Dot>> ins_own;
 
-    // dst's slots dr[0, m); sources: slots sr[sfirst[s], sfirst[s + 1]) for s in [s0, s1)
-    void plan(const SlotRef* dr, uint32_t m, const uint64_t* ok, const uint32_t* oa, const uint64_t* oc, uint32_t o,
-              uint32_t c, const SlotRef* sr, const uint32_t* sfirst, uint32_t s0, uint32_t s1) {
+    // dst's slots [f, f + m) of (dk, da, dc, dit); sources: slots
+    // [sfirst[q], sfirst[q + 1]) of (sk, sit) for q in [s0, s1)
+    void plan(const uint64_t* dk, const uint32_t* da, const uint64_t* dc, const Entries::iterator* dit, uint32_t f,
+              uint32_t m, const uint64_t* ok, const uint32_t* oa, const uint64_t* oc, uint32_t o, uint32_t c,
+              const uint64_t* sk, const Entries::iterator* sit, const uint32_t* sfirst, uint32_t s0, uint32_t s1) {
         erase.clear();
         upd.clear();
         ins.clear();
         ins_own.clear();
+        dk += f, da += f, dc += f, dit += f;
         uint32_t i = 0, j = 0;
         while (i < c || j < m) {
-            if (j < m && (i == c || dr[j].id < ok[o + i])) {
-                erase.push_back(dr[j].it);
+            if (j < m && (i == c || dk[j] < ok[o + i])) {
+                erase.push_back(dit[j]);
                 ++j;
-            } else if (j < m && dr[j].id == ok[o + i]) {
-                const Dot nd{oa[o + i], oc[o + i]};
-                if (dr[j].dot != nd) upd.emplace_back(dr[j].it, nd);
+            } else if (j < m && dk[j] == ok[o + i]) {
+                if (da[j] != oa[o + i] || dc[j] != oc[o + i]) upd.emplace_back(dit[j], Dot{oa[o + i], oc[o + i]});
                 ++i, ++j;
             } else {  // a key the destination did not hold: its string is a source's
                 const uint64_t id = ok[o + i];
                 const std::string* name = nullptr;
                 for (uint32_t q = s0; q < s1 && !name; ++q) {
-                    const SlotRef* lo = sr + sfirst[q];
-                    const SlotRef* hi = sr + sfirst[q + 1];
-                    const SlotRef* f =
-                        std::lower_bound(lo, hi, id, [](const SlotRef& x, uint64_t v) { return x.id < v; });
-                    if (f != hi && f->id == id) name = &f->it->first;
+                    const uint64_t* lo = sk + sfirst[q];
+                    const uint64_t* hi = sk + sfirst[q + 1];
+                    const uint64_t* at = std::lower_bound(lo, hi, id);
+                    if (at != hi && *at == id) name = &sit[at - sk]->first;
                 }
                 if (!name) throw Error(CRDT_E_INVALID, "merge result holds a key no state of its document had");
                 if (own)
@@ -472,12 +519,12 @@ struct Plan {
 // Destinations must be distinct; true when some source is also a destination
 // of the batch, so that every plan must be made before any map changes.
 inline bool aliased(const std::vector<AWSet*>& dsts, const std::vector<const AWSet*>& srcs, const char* what) {
-    std::unordered_map<const AWSet*, int> seen;
-    seen.reserve(dsts.size());
-    for (auto* d : dsts)
-        if (!seen.emplace(d, 0).second) throw Error(CRDT_E_INVALID, std::string(what) + ": a destination appears twice");
+    std::vector<const AWSet*> v(dsts.begin(), dsts.end());
+    std::sort(v.begin(), v.end());
+    if (std::adjacent_find(v.begin(), v.end()) != v.end())
+        throw Error(CRDT_E_INVALID, std::string(what) + ": a destination appears twice");
     for (auto* s : srcs)
-        if (seen.count(s)) return true;
+        if (std::binary_search(v.begin(), v.end(), s)) return true;
     return false;
 }
 
@@ -598,7 +645,12 @@ inline int replay_checks(int mode, const AWSet& dst, const std::vector<const AWS
 // The padded width R of a batch whose document d holds states_of(d) (dst
 // first), after the host checks of its documents with a vector shorter than R.
 template <typename F>
-size_t ragged_checks(int mode, size_t n_docs, F&& states_of, const char* what) {
+size_t ragged_checks(int mode, size_t n_docs, F&& states_of, const char* what, size_t lo_len, size_t hi_len) {
+    // every vector of the batch has one length >= 1: the kernels are exact at R
+    if (lo_len == hi_len && hi_len >= 1) {
+        if (hi_len > CRDT_MAX_R) throw Error(CRDT_E_INVALID, "version vector longer than CRDT_MAX_R");
+        return hi_len;
+    }
     size_t R = 1;
     for (size_t d = 0; d < n_docs; ++d)
         for (const AWSet* s : states_of(d)) R = std::max(R, s->versionVector.size());
@@ -704,9 +756,11 @@ inline crdt_awset_batch pack(Batch& b, Engine& e, bool tombs) {
         ta = e.pinned<uint32_t>(kS_TACT, nt);
         tc = e.pinned<uint64_t>(kS_TCTR, nt);
     }
-    std::vector<unsigned> rank_count(host_threads() + 1, 0);
+    b.dk = dk, b.da = da, b.dc = dc, b.sk = sk, b.sa = sa, b.sc = sc;
+    b.dit = e.iters(0, nd);
+    b.sit = e.iters(1, nse);
     parallel_docs(n, [&](size_t lo, size_t hi) {
-        DocPacker pk{b, dk, sk, tk, dc, sc, tc, da, sa, ta, {}, {}, {}, false};
+        DocPacker pk{b, tk, tc, ta, {}, {}, {}, false};
         for (size_t d = lo; d < hi; ++d) {
             pk.doc(d);
             const auto& v = b.dst[d]->versionVector;
@@ -743,12 +797,25 @@ inline crdt_awset_batch src_view(const Batch& b, Engine& e) {
 
 inline void set_vv(AWSet& dst, const uint64_t* vv, size_t width) { dst.versionVector.assign(vv, vv + width); }
 
+// shortest and longest VersionVector of some states
+template <typename V>
+void vv_range(const V& states, size_t& lo, size_t& hi) {
+    for (const AWSet* x : states) {
+        lo = std::min(lo, x->versionVector.size());
+        hi = std::max(hi, x->versionVector.size());
+    }
+}
+
 inline Batch join_batch(const std::vector<AWSet*>& dsts, const std::vector<const AWSet*>& srcs, const char* what) {
     if (dsts.size() != srcs.size()) throw Error(CRDT_E_INVALID, std::string(what) + ": length mismatch");
     Batch b;
     b.n_docs = dsts.size();
+    size_t lo = ~(size_t)0, hi = 0;
+    vv_range(dsts, lo, hi);
+    vv_range(srcs, lo, hi);
     b.R = ragged_checks(
-        CRDT_FOLD_AWSET, b.n_docs, [&](size_t d) { return std::vector<const AWSet*>{dsts[d], srcs[d]}; }, what);
+        CRDT_FOLD_AWSET, b.n_docs, [&](size_t d) { return std::vector<const AWSet*>{dsts[d], srcs[d]}; }, what, lo,
+        hi);
     b.dst = dsts;
     b.src = srcs;
     b.src_beg.resize(b.n_docs + 1);
@@ -775,8 +842,9 @@ inline void MergeBatch(const std::vector<AWSet*>& dsts, const std::vector<const 
     apply_docs(
         n, aliased(b.dst, b.src, "MergeBatch"),
         [&](size_t d, DocPlan& p) {
-            p.a.plan(b.dref.data() + b.dfirst[d], b.dfirst[d + 1] - b.dfirst[d], co.keys, co.actors, co.counters,
-                     co.offsets[d], co.counts[d], b.sref.data(), b.sfirst.data(), (uint32_t)d, (uint32_t)d + 1);
+            p.a.plan(b.dk, b.da, b.dc, b.dit, b.dfirst[d], b.dfirst[d + 1] - b.dfirst[d], co.keys, co.actors,
+                     co.counters, co.offsets[d], co.counts[d], b.sk, b.sit, b.sfirst.data(), (uint32_t)d,
+                     (uint32_t)d + 1);
         },
         [&](size_t d, DocPlan& p) {
             const size_t w = std::max(b.dst[d]->versionVector.size(), b.src[d]->versionVector.size());
@@ -812,10 +880,12 @@ inline void ExchangeBatch(const std::vector<AWSet*>& as, const std::vector<AWSet
     apply_docs(
         n, false,
         [&](size_t d, DocPlan& p) {  // both plans read the untouched maps ...
-            p.a.plan(b.dref.data() + b.dfirst[d], b.dfirst[d + 1] - b.dfirst[d], oab.keys, oab.actors, oab.counters,
-                     oab.offsets[d], oab.counts[d], b.sref.data(), b.sfirst.data(), (uint32_t)d, (uint32_t)d + 1);
-            p.b.plan(b.sref.data() + b.sfirst[d], b.sfirst[d + 1] - b.sfirst[d], oba.keys, oba.actors, oba.counters,
-                     oba.offsets[d], oba.counts[d], b.dref.data(), b.dfirst.data(), (uint32_t)d, (uint32_t)d + 1);
+            p.a.plan(b.dk, b.da, b.dc, b.dit, b.dfirst[d], b.dfirst[d + 1] - b.dfirst[d], oab.keys, oab.actors,
+                     oab.counters, oab.offsets[d], oab.counts[d], b.sk, b.sit, b.sfirst.data(), (uint32_t)d,
+                     (uint32_t)d + 1);
+            p.b.plan(b.sk, b.sa, b.sc, b.sit, b.sfirst[d], b.sfirst[d + 1] - b.sfirst[d], oba.keys, oba.actors,
+                     oba.counters, oba.offsets[d], oba.counts[d], b.dk, b.dit, b.dfirst.data(), (uint32_t)d,
+                     (uint32_t)d + 1);
         },
         [&](size_t d, DocPlan& p) {  // ... then each map changes
             const size_t w = std::max(as[d]->versionVector.size(), bs[d]->versionVector.size());
@@ -835,6 +905,9 @@ inline void fold(int mode, const std::vector<AWSet*>& dsts, const std::vector<st
     auto t0 = clk::now();
     Batch b;
     b.n_docs = dsts.size();
+    size_t lo = ~(size_t)0, hi = 0;
+    vv_range(dsts, lo, hi);
+    for (auto& l : srcs) vv_range(l, lo, hi);
     b.R = ragged_checks(
         mode, b.n_docs,
         [&](size_t d) {
@@ -842,7 +915,7 @@ inline void fold(int mode, const std::vector<AWSet*>& dsts, const std::vector<st
             v.insert(v.end(), srcs[d].begin(), srcs[d].end());
             return v;
         },
-        mode == CRDT_FOLD_DELTA ? "DeltaMergeBatch" : "FoldBatch");
+        mode == CRDT_FOLD_DELTA ? "DeltaMergeBatch" : "FoldBatch", lo, hi);
     b.dst = dsts;
     for (auto& l : srcs) {
         b.src.insert(b.src.end(), l.begin(), l.end());
@@ -884,8 +957,9 @@ inline void fold(int mode, const std::vector<AWSet*>& dsts, const std::vector<st
     apply_docs(
         n, aliased(b.dst, b.src, "fold"),
         [&](size_t d, DocPlan& p) {
-            p.a.plan(b.dref.data() + b.dfirst[d], b.dfirst[d + 1] - b.dfirst[d], co.keys, co.actors, co.counters,
-                     co.offsets[d], co.counts[d], b.sref.data(), b.sfirst.data(), b.src_beg[d], b.src_beg[d + 1]);
+            p.a.plan(b.dk, b.da, b.dc, b.dit, b.dfirst[d], b.dfirst[d + 1] - b.dfirst[d], co.keys, co.actors,
+                     co.counters, co.offsets[d], co.counts[d], b.sk, b.sit, b.sfirst.data(), b.src_beg[d],
+                     b.src_beg[d + 1]);
         },
         [&](size_t d, DocPlan& p) {
             const uint32_t s0 = b.src_beg[d], s1 = b.src_beg[d + 1];

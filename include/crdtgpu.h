@@ -223,6 +223,10 @@ int crdt_gen_replicas_async(crdt_ctx* ctx, uint64_t seed, uint32_t n_docs, uint3
 #define CRDT_PROBE_WRITE_PLAIN 3
 #define CRDT_PROBE_COPY_PLAIN 4
 int crdt_bw_probe(crdt_ctx* ctx, int kind, const void* a, void* b, size_t bytes, int reps, double* gbs);
+/* The shader clock (MHz) while every CU runs dependent integer chains:
+ * shader-cycle counter over the fixed-rate wall clock on one wave.  Kernels
+ * bound by instruction issue scale with it; streaming ones do not. */
+int crdt_clock_probe(crdt_ctx* ctx, double* mhz);
 
 /* ---- batched local operations: the state producers -----
  * Each document receives an ordered op list, applied to its replica state

@@ -31,6 +31,8 @@ def test_probes_rates_and_copy(torch):
             assert 500.0 < g < 12000.0, (r, w, c)  # HBM3E: well under the 8 TB/s spec + cache effects
         torch.cuda.synchronize()
         assert torch.equal(a, b)
+        mhz = eng.clock_probe()
+        assert 500.0 < mhz < 3000.0, mhz  # MI355X: up to 2400 MHz
         with pytest.raises(crdtgpu.CrdtError):
             eng.bw_probe(7, a, b, n, 1)
         with pytest.raises(crdtgpu.CrdtError):
