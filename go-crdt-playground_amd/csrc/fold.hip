@@ -57,15 +57,21 @@ namespace crdt {
 #ifndef CRDT_FOLD_DELTA_WPE
 #define CRDT_FOLD_DELTA_WPE 3  // probe builds may override (tools/fold_probe.hip)
 #endif
+// NCH: 64-tuple chunks a document may fill on this path (AWSet folds: 128
+// tuples -- fewer registers for the prefetch and the walk, so the kernel fits
+// 128 VGPRs with no spills; larger documents take the block kernel).  VCH:
+// 64-word chunks of source clocks.
 template <bool DELTA>
 struct FoldShape {
     static constexpr int WPE = DELTA ? CRDT_FOLD_DELTA_WPE : 4;
-    static constexpr int VCAP = (DELTA && CRDT_FOLD_DELTA_WPE < 4) ? 256 : 224;
+    static constexpr int NCH = DELTA ? 4 : 2;
+    static constexpr int VCH = DELTA ? 4 : 2;
+    static constexpr int VCAP = (DELTA && CRDT_FOLD_DELTA_WPE < 4) ? 256 : (DELTA ? 224 : 128);
 };
 
-template <int VCAP_>
+template <int VCAP_, int NCAP_>
 struct FoldSmem {
-    static constexpr int NCAP = 256;  // document entries + source entries + tombstones
+    static constexpr int NCAP = NCAP_;  // document entries + source entries + tombstones
     static constexpr int VCAP = VCAP_;  // sources x R clock words
     static constexpr int MCAP = 64;   // sources per document
     uint64_t tk[NCAP];        // tuple keys; compacted kept keys; after the sort: segment keys
@@ -79,6 +85,7 @@ struct FoldSmem {
     uint8_t anye[MCAP];       // step j has a changed entry
     uint8_t anyt[MCAP];       // step j has an effective tombstone
     alignas(4) uint8_t smark[NCAP];  // s + 1 where source s's entries / tombstones end (step of a tuple)
+    uint16_t dbase[256];             // dense_sort: first sorted position of each key slot
 };
 
 // Tuple tag: bits 15..8 = 0 for a document entry, (j+1)*2 for an entry of
@@ -88,9 +95,10 @@ constexpr uint32_t kPadTag = 0xFFFFu;
 
 // A document's survivors, at most 4 per lane, in key order: element q of this
 // lane goes to output position off[q] (kOOB: nothing to write).
+template <int NQ>
 struct Emit {
-    uint64_t k[4], c[4];
-    uint32_t a[4], off[4];
+    uint64_t k[NQ], c[NQ];
+    uint32_t a[NQ], off[NQ];
 };
 
 // Resolve every key of the document at once, element-parallel.  After the sort
@@ -164,16 +172,19 @@ __device__ __forceinline__ bool dense_sort(Smem& m, uint64_t (&k)[EPL], uint32_t
     hi = wave_minmax<true>(hi);
     if (hi - lo >= 256u) return false;
     uint32_t* ev = reinterpret_cast<uint32_t*>(m.tk);
-    uint16_t* base = reinterpret_cast<uint16_t*>(m.tk + 128);
-    reinterpret_cast<uint4*>(ev)[lane] = make_uint4(0u, 0u, 0u, 0u);
+    uint16_t* base = m.dbase;
+    // slot and step field are recomputed from k / t where needed (no extra
+    // registers live across the sort: the AWSet fold runs at 128 VGPRs)
+    const uint64_t bs = b + 0x80000000ull - uniform(lo);
+    static_assert(sizeof(m.tk) >= 1024, "dense_sort: tk holds the 256 slot masks");
+    ev[lane] = 0u;
+    ev[64 + lane] = 0u;
+    ev[128 + lane] = 0u;
+    ev[192 + lane] = 0u;
     wave_sync();
-    uint32_t sl[EPL], hb[EPL];
 #pragma unroll
-    for (int q = 0; q < EPL; ++q) {
-        sl[q] = (uint32_t)(k[q] - b + 0x80000000ull) - lo;
-        hb[q] = t[q] >> 8;
-        if (lane * EPL + q < n) atomicOr(&ev[sl[q] & 255u], 1u << (hb[q] & 31u));
-    }
+    for (int q = 0; q < EPL; ++q)
+        if (lane * EPL + q < n) atomicOr(&ev[(uint32_t)(k[q] - bs) & 255u], 1u << ((t[q] >> 8) & 31u));
     wave_sync();
     const uint4 e4 = reinterpret_cast<const uint4*>(ev)[lane];
     const uint32_t c0 = __popc(e4.x), c1 = __popc(e4.y), c2 = __popc(e4.z), c3 = __popc(e4.w);
@@ -185,27 +196,26 @@ __device__ __forceinline__ bool dense_sort(Smem& m, uint64_t (&k)[EPL], uint32_t
 #pragma unroll
     for (int q = 0; q < EPL; ++q) {
         if (lane * EPL + q < n) {
-            const uint32_t s = sl[q] & 255u;
-            const uint32_t pos = base[s] + __popc(ev[s] & ((1u << (hb[q] & 31u)) - 1u));
+            const uint32_t sl = (uint32_t)(k[q] - bs) & 255u;
+            const uint32_t pos = base[sl] + __popc(ev[sl] & ((1u << ((t[q] >> 8) & 31u)) - 1u));
             m.stag[pos] = (uint16_t)t[q];
-            m.smark[pos] = (uint8_t)s;
+            m.smark[pos] = (uint8_t)sl;
         }
     }
     wave_sync();
-    const uint64_t kb = b - 0x80000000ull + lo;
 #pragma unroll
     for (int q = 0; q < EPL; ++q) {
         const uint32_t i = lane * EPL + q;
         const bool valid = i < n;
         t[q] = valid ? (uint32_t)m.stag[i] : kPadTag;
-        k[q] = valid ? kb + m.smark[i] : ~0ull;
+        k[q] = valid ? bs + m.smark[i] : ~0ull;
     }
     return true;
 }
 
-template <int EPL, bool DELTA, class Smem>
+template <int EPL, bool DELTA, int NQ, class Smem>
 __device__ __forceinline__ uint32_t sort_resolve(Smem& m, uint32_t Kc, uint32_t ms, uint32_t R,
-                                                 uint64_t full_mask, uint32_t lane, uint64_t lt, Emit& e,
+                                                 uint64_t full_mask, uint32_t lane, uint64_t lt, Emit<NQ>& e,
                                                  uint32_t& err STAMP_PARAM) {
     uint64_t k[EPL];
     uint32_t t[EPL];
@@ -311,7 +321,7 @@ __device__ __forceinline__ uint32_t sort_resolve(Smem& m, uint32_t Kc, uint32_t 
     uint32_t pre = 0;
     const uint32_t tot = lane_prefix_small(ne, lt, pre);
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
+    for (int q = 0; q < NQ; ++q) {
         if (q < EPL) {
             e.k[q] = k[q];
             e.a[q] = da[q];
@@ -329,9 +339,10 @@ __device__ __forceinline__ uint32_t sort_resolve(Smem& m, uint32_t Kc, uint32_t 
 }
 
 // One document's inputs, loaded a document ahead.
+template <int NCH, int VCH>
 struct FoldPref {
-    uint64_t k[4], c[4], sv[4], dv;
-    uint32_t a[4], eo, eo2, to, to2, act;
+    uint64_t k[NCH], c[NCH], sv[VCH], dv;
+    uint32_t a[NCH], eo, eo2, to, to2, act;
 };
 
 struct DocMeta {
@@ -340,11 +351,13 @@ struct DocMeta {
 
 constexpr int kFoldWaves = 2;  // wavefronts per workgroup (independent)
 constexpr int kFoldK = 32;     // consecutive documents per wavefront
-constexpr int kFoldStores = 4 * 3 + 2;  // stores of one document's write-out (walk rounds x 3 + count + VV)
+// stores of one document's write-out: walk rounds x 3 + count + VV
+__host__ __device__ constexpr int fold_stores(int nch) { return nch * 3 + 2; }
 
 template <int K, bool DELTA>
 __global__ __launch_bounds__(kFoldWaves * 64) __attribute__((amdgpu_waves_per_eu(FoldShape<DELTA>::WPE))) void fold_pipe_kernel(BatchView dst, SrcView sb, OutView out, Work wk) {
-    using Smem = FoldSmem<FoldShape<DELTA>::VCAP>;
+    constexpr int NCH = FoldShape<DELTA>::NCH, VCH = FoldShape<DELTA>::VCH;
+    using Smem = FoldSmem<FoldShape<DELTA>::VCAP, 64 * NCH>;
     __shared__ Smem smem[kFoldWaves];
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t w = threadIdx.x >> 6;
@@ -405,9 +418,9 @@ __global__ __launch_bounds__(kFoldWaves * 64) __attribute__((amdgpu_waves_per_eu
     // Issue every load of document q (no waits): tuples [document | source
     // entries | tombstones] by per-lane address (lanes past N re-read the last
     // tuple, so no load is exec-masked), clocks and offsets by buffer loads.
-    auto prefetch = [&](FoldPref& P, const DocMeta& q) {
+    auto prefetch = [&](FoldPref<NCH, VCH>& P, const DocMeta& q) {
 #pragma unroll
-        for (int c = 0; c < 4; ++c) {
+        for (int c = 0; c < NCH; ++c) {
             if ((uint32_t)c * 64u < q.N) {
                 uint32_t i = c * 64u + lane;
                 i = i < q.N ? i : q.N - 1u;
@@ -424,7 +437,7 @@ __global__ __launch_bounds__(kFoldWaves * 64) __attribute__((amdgpu_waves_per_eu
         }
         const rsrc_t rv = make_rsrc(sb.vv + (size_t)q.s0 * R, q.ms * R * 8u);
 #pragma unroll
-        for (int c = 0; c < 4; ++c)
+        for (int c = 0; c < VCH; ++c)
             if ((uint32_t)c * 64u < q.ms * R) P.sv[c] = ld64(rv, (c * 64u + lane) * 8u);
         P.dv = ld64(make_rsrc(dst.vv + (size_t)q.d * R, R * 8u), lane * 8u);
         const rsrc_t re = make_rsrc(sb.entry_off + q.s0, (q.ms + 1u) * 4u);
@@ -438,7 +451,7 @@ __global__ __launch_bounds__(kFoldWaves * 64) __attribute__((amdgpu_waves_per_eu
         P.act = ld32(make_rsrc(sb.src_actor + q.s0, q.ms * 4u), lane * 4u);
     };
 
-    FoldPref P;
+    FoldPref<NCH, VCH> P;
     P.eo2 = P.to = P.to2 = 0;
     {
         const DocMeta q0 = meta(0);
@@ -450,7 +463,7 @@ __global__ __launch_bounds__(kFoldWaves * 64) __attribute__((amdgpu_waves_per_eu
         // for the staged registers is then exact on both paths into the loop.
         const rsrc_t none = make_rsrc(out.counts, 0u);
 #pragma unroll
-        for (int i = 0; i < kFoldStores; ++i) st32(0u, none, kOOB + 4u * i);  // distinct: not merged
+        for (int i = 0; i < fold_stores(NCH); ++i) st32(0u, none, kOOB + 4u * i);  // distinct: not merged
     }
 #pragma unroll 1
     for (uint32_t k = 0; k < cnt; ++k) {
@@ -464,13 +477,17 @@ __global__ __launch_bounds__(kFoldWaves * 64) __attribute__((amdgpu_waves_per_eu
         if (!cur.big) {
             const uint32_t N = cur.N, msR = cur.ms * R;
 #pragma unroll
-            for (int c = 0; c < 4; ++c) {
+            for (int c = 0; c < NCH; ++c) {
                 const uint32_t i = c * 64u + lane;
                 if ((uint32_t)c * 64u < N && i < N) {
                     m.tk[i] = P.k[c];
                     m.ta[i] = P.a[c];
                     m.tc[i] = P.c[c];
                 }
+            }
+#pragma unroll
+            for (int c = 0; c < VCH; ++c) {
+                const uint32_t i = c * 64u + lane;
                 if ((uint32_t)c * 64u < msR && i < msR) m.svv[i] = P.sv[c];
             }
             const uint32_t nso = from_next_lane(rl(P.eo2, 0), P.eo);
@@ -486,7 +503,7 @@ __global__ __launch_bounds__(kFoldWaves * 64) __attribute__((amdgpu_waves_per_eu
                 m.anye[lane] = 0;
                 m.anyt[lane] = 0;
             }
-            reinterpret_cast<uint32_t*>(m.smark)[lane] = 0u;
+            if (lane < Smem::NCAP / 4) reinterpret_cast<uint32_t*>(m.smark)[lane] = 0u;
             wave_sync();
             // Source s's tuples end at soffv / toffv (nondecreasing in s): mark
             // s + 1 at that position (the last source ending there), so a tuple's
@@ -511,7 +528,7 @@ __global__ __launch_bounds__(kFoldWaves * 64) __attribute__((amdgpu_waves_per_eu
         // ---- fold document k
         uint64_t vfin = 0, full_mask = 0;
         uint32_t U = 0;  // survivors
-        Emit em;
+        Emit<NCH> em;
         if (!cur.big) {
             const uint32_t n = cur.n, E = cur.E, N = cur.N, ms = cur.ms;
             // schedule: U_j, one lane per actor
@@ -548,10 +565,10 @@ __global__ __launch_bounds__(kFoldWaves * 64) __attribute__((amdgpu_waves_per_eu
             STAMP(2)
             // classify the tuples: kind, step, changed / effective
             const uint32_t NQ = (N + 63u) >> 6;
-            uint32_t step[4];
-            bool isE[4], isT[4];
+            uint32_t step[NCH];
+            bool isE[NCH], isT[NCH];
 #pragma unroll
-            for (int c = 0; c < 4; ++c) {
+            for (int c = 0; c < NCH; ++c) {
                 const uint32_t i = c * 64u + lane;
                 isE[c] = i >= n && i < n + E;
                 isT[c] = i >= n + E && i < N;
@@ -565,7 +582,7 @@ __global__ __launch_bounds__(kFoldWaves * 64) __attribute__((amdgpu_waves_per_eu
                 const uint32_t c0 = n >> 6;  // first chunk holding a source tuple
                 uint32_t carry = 0;
 #pragma unroll
-                for (int c = 0; c < 4; ++c) {
+                for (int c = 0; c < NCH; ++c) {
                     if ((uint32_t)c >= c0 && (uint32_t)c < NQ) {
                         const uint32_t i = c * 64u + lane;
                         uint32_t x = ((isT[c] ? 2u : (isE[c] ? 1u : 0u)) << 8) | m.smark[i];
@@ -595,10 +612,10 @@ __global__ __launch_bounds__(kFoldWaves * 64) __attribute__((amdgpu_waves_per_eu
                 cmax = (uint32_t)__builtin_amdgcn_readlane((int)cmax, 63);  // ... whose last lane has the maximum
             }
             STAMP(11)
-            uint64_t key[4];
+            uint64_t key[NCH];
             uint32_t flag = 0, perr = 0;  // flag bit c: changed entry / effective tombstone
 #pragma unroll
-            for (int c = 0; c < 4; ++c) {
+            for (int c = 0; c < NCH; ++c) {
                 key[c] = 0;
                 if ((uint32_t)c < NQ) {
                     const uint32_t i = c * 64u + lane;
@@ -655,7 +672,7 @@ __global__ __launch_bounds__(kFoldWaves * 64) __attribute__((amdgpu_waves_per_eu
                     if (!full) {
                         bool any = false;
 #pragma unroll
-                        for (int c = 0; c < 4; ++c) {
+                        for (int c = 0; c < NCH; ++c) {
                             if ((uint32_t)c < NQ) {
                                 const uint32_t i = c * 64u + lane;
                                 const bool mine = isE[c] && step[c] == j;
@@ -681,7 +698,7 @@ __global__ __launch_bounds__(kFoldWaves * 64) __attribute__((amdgpu_waves_per_eu
                 // entries take their rebuilt bits, tombstones keep their effective bits
                 uint32_t tb = 0;
 #pragma unroll
-                for (int c = 0; c < 4; ++c) tb |= isT[c] ? (flag & (1u << c)) : 0u;
+                for (int c = 0; c < NCH; ++c) tb |= isT[c] ? (flag & (1u << c)) : 0u;
                 flag = fe | tb;
                 wave_sync();
             }
@@ -689,7 +706,7 @@ __global__ __launch_bounds__(kFoldWaves * 64) __attribute__((amdgpu_waves_per_eu
             // keep + tag, compacted in place over m.tk (every read of m.tk is done)
             uint32_t Kc = 0;
 #pragma unroll
-            for (int c = 0; c < 4; ++c) {
+            for (int c = 0; c < NCH; ++c) {
                 if ((uint32_t)c < NQ) {
                     const uint32_t i = c * 64u + lane;
                     const uint32_t j = step[c] & 63u;
@@ -710,9 +727,13 @@ __global__ __launch_bounds__(kFoldWaves * 64) __attribute__((amdgpu_waves_per_eu
             }
             wave_sync();
             STAMP(4)
-            U = Kc <= 64    ? sort_resolve<1, DELTA>(m, Kc, ms, R, full_mask, lane, lt, em, err STAMP_ARGS)
-                : Kc <= 128 ? sort_resolve<2, DELTA>(m, Kc, ms, R, full_mask, lane, lt, em, err STAMP_ARGS)
-                            : sort_resolve<4, DELTA>(m, Kc, ms, R, full_mask, lane, lt, em, err STAMP_ARGS);
+            if constexpr (NCH == 4)
+                U = Kc <= 64    ? sort_resolve<1, DELTA>(m, Kc, ms, R, full_mask, lane, lt, em, err STAMP_ARGS)
+                    : Kc <= 128 ? sort_resolve<2, DELTA>(m, Kc, ms, R, full_mask, lane, lt, em, err STAMP_ARGS)
+                                : sort_resolve<4, DELTA>(m, Kc, ms, R, full_mask, lane, lt, em, err STAMP_ARGS);
+            else
+                U = Kc <= 64 ? sort_resolve<1, DELTA>(m, Kc, ms, R, full_mask, lane, lt, em, err STAMP_ARGS)
+                             : sort_resolve<2, DELTA>(m, Kc, ms, R, full_mask, lane, lt, em, err STAMP_ARGS);
             STAMP(5)
         }
         // ---- write the survivors (every store unconditional)
@@ -722,11 +743,11 @@ __global__ __launch_bounds__(kFoldWaves * 64) __attribute__((amdgpu_waves_per_eu
                      oc = make_rsrc(out.counters + obase, capo * 8u);
         if (cur.big) {
 #pragma unroll
-            for (int q = 0; q < 4; ++q) em.off[q] = kOOB;
+            for (int q = 0; q < NCH; ++q) em.off[q] = kOOB;
             U = 0;
         }
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
+        for (int q = 0; q < NCH; ++q) {
             const uint32_t o = em.off[q];
             const uint32_t o8 = o == kOOB ? kOOB : o * 8u, o4 = o == kOOB ? kOOB : o * 4u;
             st64<kAuxNT>(em.k[q], ok, o8);

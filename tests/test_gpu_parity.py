@@ -641,3 +641,65 @@ def test_max_doc_entries_promise_is_checked(eng):
         eng.set_max_doc_entries()
     rc, want = oracle.join(dst, src)
     assert_same(eng.join(dst, src), want, 1, R)
+
+
+@pytest.mark.parametrize("kind", ["fold_delta", "join_tiles"])
+def test_graph_replay_stress_worklist_paths(torch, kind):
+    """The paths that share the worklist (push_work / work_total) and the
+    per-call counters zeroed by reset_work_kernel, captured ONCE into a HIP
+    graph and replayed 30 times, the outputs poisoned before every replay and
+    checked bit-exactly against the oracle after each: a fold whose documents
+    go to both the wave pipeline and the block kernel, and a join whose large
+    documents go through the tile plan (count / scan / split / look-back).
+    (The round-1 fold fault under replay was in a kernel since replaced; this
+    pins the shared machinery under repeated replay.)"""
+    rng = random.Random(91 if kind == "fold_delta" else 92)
+    R = 4
+    dev = torch.device("cuda:0")
+    e = crdtgpu.Engine(0)
+    try:
+        if kind == "fold_delta":
+            dsts, per_doc = [], []
+            for d in range(900):
+                big = d % 97 == 0  # > 256 tuples: the block kernel's worklist
+                dsts.append(random_state(rng, R, rng.randint(200, 600) if big else rng.randint(0, 60), 4000, 9))
+                srcs = []
+                for _ in range(rng.randint(0, 6)):
+                    ents = random_state(rng, R, rng.randint(0, 30), 4000, 12)
+                    tom = random_state(rng, R, rng.randint(0, 4), 4000, 12)[0]
+                    srcs.append((rng.randrange(R), [rng.randint(1, 12) for _ in range(R)], ents[0], tom))
+                per_doc.append(srcs)
+            hd, hs = batch_of(R, dsts), src_batch_of(R, per_doc)
+            rc, want = oracle.fold(CRDT_FOLD_DELTA, hd, hs)
+            assert rc == 0
+            dd, ds = hd.to(dev), hs.to(dev)
+            out = OutBuffers(hd.n_docs, R, hs.out_slots(hd), device=dev)
+            e.reserve(hd.n_docs, out.slots)
+
+            def call(s):
+                e.fold_async(CRDT_FOLD_DELTA, dd, ds, out, stream=s)
+        else:
+            a, b = join_case(rng, 400, R, lambda: rng.choice([0, 3, 64, 65, 900, 5000]), 20000, 9)
+            rc, want = oracle.join(a, b)
+            assert rc == 0
+            dd, ds = a.to(dev), b.to(dev)
+            out = OutBuffers(a.n_docs, R, int(a.offsets[-1]) + int(b.offsets[-1]), device=dev)
+            e.set_option("join_tile_capacity", 1 << 16)
+
+            def call(s):
+                e.join_async(dd, ds, out, stream=s)
+        s = torch.cuda.current_stream()
+        call(s)  # eager first: sizes every workspace
+        e.sync(s)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            call(torch.cuda.current_stream())
+        n = want.n_docs if hasattr(want, "n_docs") else len(want.counts)
+        for _ in range(30):
+            for t in (out.keys, out.actors, out.counters, out.vv, out.counts, out.offsets):
+                t.fill_(-1)
+            g.replay()
+            e.sync(s)
+            assert_same_all(host_out(out, torch), want, n, R)
+    finally:
+        e.close()
