@@ -175,7 +175,7 @@ __device__ __forceinline__ bool dense_sort(Smem& m, uint64_t (&k)[EPL], uint32_t
     uint16_t* base = m.dbase;
     // slot and step field are recomputed from k / t where needed (no extra
     // registers live across the sort: the AWSet fold runs at 128 VGPRs)
-    const uint64_t bs = b + 0x80000000ull - uniform(lo);
+    const uint64_t bs = b - 0x80000000ull + uniform(lo);  // key of slot 0
     static_assert(sizeof(m.tk) >= 1024, "dense_sort: tk holds the 256 slot masks");
     ev[lane] = 0u;
     ev[64 + lane] = 0u;
