@@ -140,12 +140,17 @@ enum Pin {
 };
 }  // namespace detail
 
-// One context per host thread (crdt_ctx), plus the page-locked staging its
-// batch calls reuse.
+namespace detail {
+struct Batch;
+}
+
+// One context per host thread (crdt_ctx), plus the page-locked staging and
+// the host scratch its batch calls reuse (nothing large is allocated or freed
+// per call).
 class Engine {
    public:
-    explicit Engine(int device = 0) { check(crdt_ctx_create(device, &ctx_), "crdt_ctx_create"); }
-    ~Engine() { crdt_ctx_destroy(ctx_); }
+    explicit Engine(int device = 0);
+    ~Engine();
     Engine(const Engine&) = delete;
     Engine& operator=(const Engine&) = delete;
     crdt_ctx* ctx() const { return ctx_; }
@@ -164,10 +169,13 @@ class Engine {
         return its_[role].data();
     }
 
+    detail::Batch& batch() { return *batch_; }
+
    private:
     crdt_ctx* ctx_ = nullptr;
     detail::PinnedBuf pin_[detail::kPinSlots];
     std::vector<Entries::iterator> its_[2];
+    detail::Batch* batch_ = nullptr;
 };
 
 class AWSetDelta;
@@ -242,7 +250,7 @@ class AWSetDelta : public AWSet {
 
 // Seconds per phase of the last batch call on this thread (boundary cost).
 struct BoundaryStats {
-    double pack_s = 0, device_s = 0, apply_s = 0;
+    double pack_s = 0, device_s = 0, apply_s = 0, call_s = 0;
     size_t rank_docs = 0;  // documents interned by rank after a hash collision
 };
 inline BoundaryStats& LastStats() {
@@ -344,34 +352,103 @@ struct Batch {
     uint64_t *dk = nullptr, *dc = nullptr, *sk = nullptr, *sc = nullptr;
     uint32_t *da = nullptr, *sa = nullptr;
     Entries::iterator *dit = nullptr, *sit = nullptr;
+    void reset() {  // keeps every vector's capacity
+        R = 1;
+        n_docs = 0;
+        dst.clear();
+        src.clear();
+        src_beg.assign(1, 0);
+    }
 };
 
-// Fill doc d's slots: ids (hash, or ranks after a collision), sorted per
-// state, written to the page-locked SoA arrays and to the iterator arrays.
+}  // namespace detail
+
+inline Engine::Engine(int device) : batch_(new detail::Batch()) {
+    const int rc = crdt_ctx_create(device, &ctx_);
+    if (rc != CRDT_OK) {
+        delete batch_;
+        throw Error(rc, "crdt_ctx_create");
+    }
+}
+inline Engine::~Engine() {
+    crdt_ctx_destroy(ctx_);
+    delete batch_;
+}
+
+namespace detail {
+
+// Fill doc d's slots.  A document's key ids are the order in which its keys
+// first appear over its states (the destination's keys in map order, then
+// each new key of each source): exact -- keys are matched by string, through
+// a small per-document open-addressing table of (hash, key) -- and small, so
+// every state is placed in ascending id order by direct addressing, with no
+// comparison sort.  The destination's ids are its map order, already
+// ascending.  (CRDT_HOST_RANK_IDS=1 instead gives the keys' ranks in string
+// order, the fallback path of the earlier hash-id scheme, kept for tests.)
 struct DocPacker {
     Batch& b;
     uint64_t* tk;
     uint64_t* tc;
     uint32_t* ta;
-    std::vector<std::pair<uint64_t, const std::string*>> names;  // thread-local scratch
-    std::vector<const std::string*> sorted;                      // rank fallback scratch
-    std::vector<SlotRef> tmp;
-    bool clash = false;
 
+    struct Cell {
+        uint64_t h;
+        const std::string* key;
+        uint32_t id, gen;
+    };
+    std::vector<Cell> cells;
+    uint32_t mask = 0, gen = 0, next = 0;
+    std::vector<Entries::iterator> by_id;  // scratch: a state's element per id (or end)
+    std::vector<uint8_t> has;
+    std::vector<const std::string*> sorted;
+
+    uint32_t intern(const std::string& k) {
+        const uint64_t h = key_hash(k);
+        for (uint32_t i = (uint32_t)h & mask;; i = (i + 1) & mask) {
+            Cell& c = cells[i];
+            if (c.gen != gen) {
+                c = Cell{h, &k, next, gen};
+                return next++;
+            }
+            if (c.h == h && *c.key == k) return c.id;
+        }
+    }
+    void begin_doc(size_t n_keys) {
+        size_t cap = 64;
+        while (cap < 2 * n_keys) cap <<= 1;
+        if (cells.size() < cap) cells.assign(cap, Cell{0, nullptr, 0, 0}), gen = 0;
+        mask = (uint32_t)cap - 1;
+        if (++gen == 0) {  // generation wrap: clear once
+            std::fill(cells.begin(), cells.end(), Cell{0, nullptr, 0, 0});
+            gen = 1;
+        }
+        next = 0;
+    }
+    // One state: ids via `id_of`, written in ascending id order (direct
+    // addressing over the ids given out so far).
     template <typename IdOf>
     void put_state(const Entries& m, uint32_t first, uint64_t* k, uint32_t* a, uint64_t* c, Entries::iterator* its,
                    IdOf&& id_of) {
-        tmp.clear();
-        for (auto it = const_cast<Entries&>(m).begin(); it != m.end(); ++it)
-            tmp.push_back(SlotRef{id_of(it->first), it->second, it});
-        std::sort(tmp.begin(), tmp.end(), [](const SlotRef& x, const SlotRef& y) { return x.id < y.id; });
-        for (size_t i = 0; i < tmp.size(); ++i) {
-            k[first + i] = tmp[i].id;
-            a[first + i] = tmp[i].dot.actor;
-            c[first + i] = tmp[i].dot.counter;
-            if (its) its[first + i] = tmp[i].it;
-            // two keys of one state with one id: a collision (keys of a map are distinct)
-            if (i && tmp[i].id == tmp[i - 1].id) clash = true;
+        const Entries::iterator end = const_cast<Entries&>(m).end();
+        for (auto it = const_cast<Entries&>(m).begin(); it != end; ++it) {
+            const uint32_t id = id_of(it->first);
+            if (id >= by_id.size()) {
+                by_id.resize(id + 1 + id / 2);
+                has.resize(by_id.size(), 0);
+            }
+            by_id[id] = it;
+            has[id] = 1;
+        }
+        const uint32_t stop = first + (uint32_t)m.size();
+        for (uint32_t id = 0, o = first; o < stop; ++id) {
+            if (!has[id]) continue;
+            has[id] = 0;
+            const Entries::iterator it = by_id[id];
+            k[o] = id;
+            a[o] = it->second.actor;
+            c[o] = it->second.counter;
+            if (its) its[o] = it;
+            ++o;
         }
     }
     template <typename IdOf>
@@ -383,43 +460,18 @@ struct DocPacker {
                 if (auto* del = b.src[s]->deleted_map()) put_state(*del, b.tfirst[s], tk, ta, tc, nullptr, id_of);
         }
     }
-    // Across states: equal ids must be equal strings.  Two states (a join): a
-    // merge of the two sorted id runs; more (a fold, or tombstones): one sort.
-    bool cross_clash(size_t d) {
-        const uint32_t s0 = b.src_beg[d], s1 = b.src_beg[d + 1];
-        const bool has_tombs = tk && b.tfirst[s1] > b.tfirst[s0];
-        if (s1 - s0 == 1 && !has_tombs) {
-            const uint64_t* x = b.dk + b.dfirst[d];
-            const uint64_t* y = b.sk + b.sfirst[s0];
-            const uint32_t nx = b.dfirst[d + 1] - b.dfirst[d], ny = b.sfirst[s0 + 1] - b.sfirst[s0];
-            for (uint32_t i = 0, j = 0; i < nx && j < ny;) {
-                if (x[i] < y[j]) {
-                    ++i;
-                } else if (y[j] < x[i]) {
-                    ++j;
-                } else {
-                    if (b.dit[b.dfirst[d] + i]->first != b.sit[b.sfirst[s0] + j]->first) return true;
-                    ++i, ++j;
-                }
-            }
-            return false;
-        }
-        names.clear();
-        for (uint32_t i = b.dfirst[d]; i < b.dfirst[d + 1]; ++i) names.emplace_back(b.dk[i], &b.dit[i]->first);
-        for (uint32_t i = b.sfirst[s0]; i < b.sfirst[s1]; ++i) names.emplace_back(b.sk[i], &b.sit[i]->first);
-        if (has_tombs)
-            for (uint32_t s = s0; s < s1; ++s)
-                if (auto* del = b.src[s]->deleted_map())
-                    for (auto& kv : *del) names.emplace_back(key_hash(kv.first), &kv.first);
-        std::sort(names.begin(), names.end(), [](const auto& x, const auto& y) { return x.first < y.first; });
-        for (size_t i = 1; i < names.size(); ++i)
-            if (names[i].first == names[i - 1].first && *names[i].second != *names[i - 1].second) return true;
-        return false;
-    }
     void doc(size_t d) {
-        clash = false;
-        put_doc(d, [](const std::string& k) { return key_hash(k); });
-        if (!clash && !force_rank_ids() && !cross_clash(d)) return;
+        if (!force_rank_ids()) {
+            size_t n_keys = b.dst[d]->entries.size();
+            for (uint32_t s = b.src_beg[d]; s < b.src_beg[d + 1]; ++s) {
+                n_keys += b.src[s]->entries.size();
+                if (tk)
+                    if (auto* del = b.src[s]->deleted_map()) n_keys += del->size();
+            }
+            begin_doc(n_keys);
+            put_doc(d, [this](const std::string& k) { return intern(k); });
+            return;
+        }
         // rank ids: the key's rank in string order over the doc's states
         b.rank_doc[d] = 1;
         sorted.clear();
@@ -434,8 +486,9 @@ struct DocPacker {
         auto lt = [](const std::string* x, const std::string* y) { return *x < *y; };
         std::sort(sorted.begin(), sorted.end(), lt);
         sorted.erase(std::unique(sorted.begin(), sorted.end(), [](auto* x, auto* y) { return *x == *y; }), sorted.end());
+        next = (uint32_t)sorted.size();
         put_doc(d, [&](const std::string& k) {
-            return (uint64_t)(std::lower_bound(sorted.begin(), sorted.end(), &k, lt) - sorted.begin());
+            return (uint32_t)(std::lower_bound(sorted.begin(), sorted.end(), &k, lt) - sorted.begin());
         });
     }
 };
@@ -480,6 +533,8 @@ struct Plan {
         ins_own.clear();
         dk += f, da += f, dc += f, dit += f;
         uint32_t i = 0, j = 0;
+        uint32_t js = sfirst[s0];  // one source: its slots are walked along the output (both sorted)
+        const bool one = s1 - s0 == 1;
         while (i < c || j < m) {
             if (j < m && (i == c || dk[j] < ok[o + i])) {
                 erase.push_back(dit[j]);
@@ -490,7 +545,12 @@ struct Plan {
             } else {  // a key the destination did not hold: its string is a source's
                 const uint64_t id = ok[o + i];
                 const std::string* name = nullptr;
-                for (uint32_t q = s0; q < s1 && !name; ++q) {
+                if (one) {
+                    const uint32_t je = sfirst[s0 + 1];
+                    while (js < je && sk[js] < id) ++js;
+                    if (js < je && sk[js] == id) name = &sit[js]->first;
+                }
+                for (uint32_t q = s0; q < s1 && !name && !one; ++q) {
                     const uint64_t* lo = sk + sfirst[q];
                     const uint64_t* hi = sk + sfirst[q + 1];
                     const uint64_t* at = std::lower_bound(lo, hi, id);
@@ -509,7 +569,8 @@ struct Plan {
         for (auto it : erase) dst.entries.erase(it);
         for (auto& u : upd) u.first->second = u.second;
         if (!ins.empty() || !ins_own.empty()) {
-            dst.entries.reserve(dst.entries.size() + ins.size() + ins_own.size());
+            // no reserve(): libstdc++'s rehash(n) also SHRINKS to n's bucket
+            // count, relinking every node; inserts grow the table only when needed
             for (auto& x : ins) dst.entries.emplace(*x.first, x.second);
             for (auto& x : ins_own) dst.entries.emplace(std::move(x.first), x.second);
         }
@@ -760,7 +821,7 @@ inline crdt_awset_batch pack(Batch& b, Engine& e, bool tombs) {
     b.dit = e.iters(0, nd);
     b.sit = e.iters(1, nse);
     parallel_docs(n, [&](size_t lo, size_t hi) {
-        DocPacker pk{b, tk, tc, ta, {}, {}, {}, false};
+        DocPacker pk{b, tk, tc, ta, {}, 0, 0, 0, {}, {}, {}};
         for (size_t d = lo; d < hi; ++d) {
             pk.doc(d);
             const auto& v = b.dst[d]->versionVector;
@@ -806,9 +867,11 @@ void vv_range(const V& states, size_t& lo, size_t& hi) {
     }
 }
 
-inline Batch join_batch(const std::vector<AWSet*>& dsts, const std::vector<const AWSet*>& srcs, const char* what) {
+template <typename SrcVec>
+Batch& join_batch(Engine& e, const std::vector<AWSet*>& dsts, const SrcVec& srcs, const char* what) {
     if (dsts.size() != srcs.size()) throw Error(CRDT_E_INVALID, std::string(what) + ": length mismatch");
-    Batch b;
+    Batch& b = e.batch();
+    b.reset();
     b.n_docs = dsts.size();
     size_t lo = ~(size_t)0, hi = 0;
     vv_range(dsts, lo, hi);
@@ -816,8 +879,8 @@ inline Batch join_batch(const std::vector<AWSet*>& dsts, const std::vector<const
     b.R = ragged_checks(
         CRDT_FOLD_AWSET, b.n_docs, [&](size_t d) { return std::vector<const AWSet*>{dsts[d], srcs[d]}; }, what, lo,
         hi);
-    b.dst = dsts;
-    b.src = srcs;
+    b.dst.assign(dsts.begin(), dsts.end());
+    b.src.assign(srcs.begin(), srcs.end());
     b.src_beg.resize(b.n_docs + 1);
     for (size_t d = 0; d <= b.n_docs; ++d) b.src_beg[d] = (uint32_t)d;
     return b;
@@ -830,7 +893,7 @@ inline void MergeBatch(const std::vector<AWSet*>& dsts, const std::vector<const 
     using namespace detail;
     if (dsts.empty() && srcs.empty()) return;
     auto t0 = clk::now();
-    Batch b = join_batch(dsts, srcs, "MergeBatch");
+    Batch& b = join_batch(e, dsts, srcs, "MergeBatch");
     const crdt_awset_batch cd = pack(b, e, false), cs = src_view(b, e);
     const size_t n = b.n_docs, slots = (size_t)b.dfirst[n] + b.sfirst[n];
     const crdt_awset_out co = out_arrays(e, kO_OFF, n, b.R, slots);
@@ -863,7 +926,8 @@ inline void ExchangeBatch(const std::vector<AWSet*>& as, const std::vector<AWSet
     using namespace detail;
     if (as.empty() && bs.empty()) return;
     auto t0 = clk::now();
-    Batch b = join_batch(as, std::vector<const AWSet*>(bs.begin(), bs.end()), "ExchangeBatch");
+    const auto t_call = t0;
+    Batch& b = join_batch(e, as, bs, "ExchangeBatch");
     const crdt_awset_batch ca = pack(b, e, false), cb = src_view(b, e);
     const size_t n = b.n_docs, slots = (size_t)b.dfirst[n] + b.sfirst[n];
     const crdt_awset_out oab = out_arrays(e, kO_OFF, n, b.R, slots), oba = out_arrays(e, kP_OFF, n, b.R, slots);
@@ -895,6 +959,7 @@ inline void ExchangeBatch(const std::vector<AWSet*>& as, const std::vector<AWSet
             set_vv(*bs[d], oba.vv + d * b.R, w);
         });
     LastStats().apply_s = secs_since(t0);
+    LastStats().call_s = secs_since(t_call);
 }
 
 namespace detail {
@@ -903,7 +968,8 @@ inline void fold(int mode, const std::vector<AWSet*>& dsts, const std::vector<st
     if (dsts.size() != srcs.size()) throw Error(CRDT_E_INVALID, "fold: length mismatch");
     if (dsts.empty()) return;
     auto t0 = clk::now();
-    Batch b;
+    Batch& b = e.batch();
+    b.reset();
     b.n_docs = dsts.size();
     size_t lo = ~(size_t)0, hi = 0;
     vv_range(dsts, lo, hi);
@@ -916,7 +982,7 @@ inline void fold(int mode, const std::vector<AWSet*>& dsts, const std::vector<st
             return v;
         },
         mode == CRDT_FOLD_DELTA ? "DeltaMergeBatch" : "FoldBatch", lo, hi);
-    b.dst = dsts;
+    b.dst.assign(dsts.begin(), dsts.end());
     for (auto& l : srcs) {
         b.src.insert(b.src.end(), l.begin(), l.end());
         b.src_beg.push_back((uint32_t)b.src.size());
