@@ -213,6 +213,101 @@ __device__ __forceinline__ bool dense_sort(Smem& m, uint64_t (&k)[EPL], uint32_t
     return true;
 }
 
+// The AWSet fold (every step a full (*AWSet).Merge, awset.go:107-161)
+// replayed per key slot when the document's keys span fewer than 64 ids and it
+// has at most 15 sources: lane s owns key kmin + s and walks the steps in
+// order, the key's state (present, dot) in registers -- the reference's rule
+// one key at a time:
+//   key in source j:  present -> dot := the source's dot (awset.go:123-129,142)
+//                     absent  -> added iff !HasDot(V_j, dot) (:133-140)
+//   not in source j:  present -> removed iff HasDot(svv_j, dot) (:146-158)
+// V_j is the clock before step j (the schedule's prefix max: an AWSet fold has
+// no no-op steps).  HasDot is evaluated exactly where Go evaluates it, so
+// actor == R flags exactly the reference's panics.  Tables alias tk and stag
+// (dead once the keys are in registers): mask[row] = the slots present in a
+// row (row 0 the document, row j + 1 source j), idx[row * 64 + slot] = the
+// tuple.  Survivors come out in slot = key order, one store round.  Returns
+// false (nothing changed) when the document does not qualify.
+template <int NCH, class Smem>
+__device__ __forceinline__ bool dense_awset_walk(Smem& m, const uint64_t (&key)[NCH], const uint32_t (&step)[NCH],
+                                                 uint32_t N, uint32_t n, uint32_t ms, uint32_t R, uint32_t lane,
+                                                 uint64_t lt, Emit<NCH>& e, uint32_t& U, uint32_t& err) {
+    static_assert(sizeof(m.tk) >= 16 * 64 && sizeof(m.stag) >= 16 * 8, "dense_awset_walk: table space");
+    if (N == 0 || ms > 15) return false;
+    const uint64_t b = readlane64(key[0], 0);  // element 0 is valid
+    bool bad = false;
+    uint32_t lo = ~0u, hi = 0u;
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+        const bool valid = c * 64u + lane < N;
+        const uint64_t d = key[c] - b + 0x80000000ull;
+        bad |= valid && (d >> 32) != 0;
+        lo = valid ? min(lo, (uint32_t)d) : lo;
+        hi = valid ? max(hi, (uint32_t)d) : hi;
+    }
+    if (ballot(bad)) return false;
+    lo = wave_minmax<false>(lo);
+    hi = wave_minmax<true>(hi);
+    if (hi - lo >= 64u) return false;
+    const uint64_t kb = b - 0x80000000ull + lo;  // key of slot 0
+    uint64_t* mask = reinterpret_cast<uint64_t*>(m.stag);
+    uint8_t* idx = reinterpret_cast<uint8_t*>(m.tk);
+    if (lane <= ms) mask[lane] = 0ull;
+    wave_sync();
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+        const uint32_t i = c * 64u + lane;
+        if (i < N) {
+            const uint32_t sl = (uint32_t)(key[c] - kb) & 63u;
+            const uint32_t row = i < n ? 0u : (step[c] & 63u) + 1u;
+            atomicOr(reinterpret_cast<unsigned long long*>(&mask[row]), 1ull << sl);
+            idx[row * 64u + sl] = (uint8_t)i;
+        }
+    }
+    wave_sync();
+    bool P = (mask[0] >> lane) & 1ull;
+    uint32_t da = 0;
+    uint64_t dc = 0;
+    if (P) {
+        const uint32_t t = idx[lane];
+        da = m.ta[t];
+        dc = m.tc[t];
+    }
+    uint32_t perr = 0;
+    for (uint32_t j = 0; j < ms; ++j) {
+        const bool has = (mask[j + 1] >> lane) & 1ull;
+        if (has) {
+            const uint32_t t = idx[(j + 1) * 64u + lane];
+            const uint32_t ea = m.ta[t];
+            const uint64_t ec = m.tc[t];
+            if (!P) {  // src-only: HasDot(dstVV, s), awset.go:133
+                perr |= ea == R ? 1u : 0u;
+                P = !(ea < R && m.vs[j * R + ea] >= ec);
+            }
+            da = ea;  // the source's dot wins when present (an absent key's dot is never read)
+            dc = ec;
+        } else if (P) {  // dst-only: HasDot(srcVV, d), awset.go:152
+            perr |= da == R ? 1u : 0u;
+            P = !(da < R && m.svv[j * R + da] >= dc);
+        }
+    }
+    if (perr) err |= kErrActorRange;
+    const uint64_t pm = ballot(P);
+    U = popc(pm);
+    e.k[0] = kb + lane;
+    e.a[0] = da;
+    e.c[0] = dc;
+    e.off[0] = P ? popc(pm & lt) : kOOB;
+#pragma unroll
+    for (int q = 1; q < NCH; ++q) {
+        e.k[q] = 0;
+        e.a[q] = 0;
+        e.c[q] = 0;
+        e.off[q] = kOOB;
+    }
+    return true;
+}
+
 template <int EPL, bool DELTA, int NQ, class Smem>
 __device__ __forceinline__ uint32_t sort_resolve(Smem& m, uint32_t Kc, uint32_t ms, uint32_t R,
                                                  uint64_t full_mask, uint32_t lane, uint64_t lt, Emit<NQ>& e,
@@ -703,6 +798,9 @@ __global__ __launch_bounds__(kFoldWaves * 64) __attribute__((amdgpu_waves_per_eu
                 wave_sync();
             }
             err |= perr;
+            bool walked = false;
+            if constexpr (!DELTA) walked = dense_awset_walk<NCH>(m, key, step, N, n, ms, R, lane, lt, em, U, err);
+            if (!walked) {
             // keep + tag, compacted in place over m.tk (every read of m.tk is done)
             uint32_t Kc = 0;
 #pragma unroll
@@ -734,6 +832,7 @@ __global__ __launch_bounds__(kFoldWaves * 64) __attribute__((amdgpu_waves_per_eu
             else
                 U = Kc <= 64 ? sort_resolve<1, DELTA>(m, Kc, ms, R, full_mask, lane, lt, em, err STAMP_ARGS)
                              : sort_resolve<2, DELTA>(m, Kc, ms, R, full_mask, lane, lt, em, err STAMP_ARGS);
+            }
             STAMP(5)
         }
         // ---- write the survivors (every store unconditional)

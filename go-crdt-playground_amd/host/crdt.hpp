@@ -348,7 +348,9 @@ struct Batch {
     std::vector<uint32_t> src_beg{0};          // doc d's sources: [src_beg[d], src_beg[d+1])
     std::vector<uint32_t> dfirst, sfirst;      // per state: first slot (prefix of entry counts)
     std::vector<uint32_t> tfirst;              // per source: first tombstone slot
-    std::vector<uint8_t> rank_doc;             // 1: ids of doc d are ranks (hash collision)
+    std::vector<uint8_t> rank_doc;             // 1: ids of doc d are ranks (CRDT_HOST_RANK_IDS)
+    std::vector<AWSet*> all;                   // scratch of the aliasing check
+    std::vector<const AWSet*> sorted_states;   // scratch of the aliasing check
     uint64_t *dk = nullptr, *dc = nullptr, *sk = nullptr, *sc = nullptr;
     uint32_t *da = nullptr, *sa = nullptr;
     Entries::iterator *dit = nullptr, *sit = nullptr;
@@ -579,8 +581,9 @@ struct Plan {
 
 // Destinations must be distinct; true when some source is also a destination
 // of the batch, so that every plan must be made before any map changes.
-inline bool aliased(const std::vector<AWSet*>& dsts, const std::vector<const AWSet*>& srcs, const char* what) {
-    std::vector<const AWSet*> v(dsts.begin(), dsts.end());
+inline bool aliased(const std::vector<AWSet*>& dsts, const std::vector<const AWSet*>& srcs, const char* what,
+                    std::vector<const AWSet*>& v) {
+    v.assign(dsts.begin(), dsts.end());
     std::sort(v.begin(), v.end());
     if (std::adjacent_find(v.begin(), v.end()) != v.end())
         throw Error(CRDT_E_INVALID, std::string(what) + ": a destination appears twice");
@@ -903,7 +906,7 @@ inline void MergeBatch(const std::vector<AWSet*>& dsts, const std::vector<const 
     LastStats().device_s = secs_since(t0);
     t0 = clk::now();
     apply_docs(
-        n, aliased(b.dst, b.src, "MergeBatch"),
+        n, aliased(b.dst, b.src, "MergeBatch", b.sorted_states),
         [&](size_t d, DocPlan& p) {
             p.a.plan(b.dk, b.da, b.dc, b.dit, b.dfirst[d], b.dfirst[d + 1] - b.dfirst[d], co.keys, co.actors,
                      co.counters, co.offsets[d], co.counts[d], b.sk, b.sit, b.sfirst.data(), (uint32_t)d,
@@ -937,9 +940,10 @@ inline void ExchangeBatch(const std::vector<AWSet*>& as, const std::vector<AWSet
     LastStats().device_s = secs_since(t0);
     t0 = clk::now();
     {
-        std::vector<AWSet*> all(as);
+        std::vector<AWSet*>& all = e.batch().all;  // reused scratch: no large free inside the call
+        all.assign(as.begin(), as.end());
         all.insert(all.end(), bs.begin(), bs.end());
-        aliased(all, {}, "ExchangeBatch");  // every state distinct: no document reads another's map
+        aliased(all, {}, "ExchangeBatch", e.batch().sorted_states);  // every state distinct
     }
     apply_docs(
         n, false,
@@ -1021,7 +1025,7 @@ inline void fold(int mode, const std::vector<AWSet*>& dsts, const std::vector<st
     LastStats().device_s = secs_since(t0);
     t0 = clk::now();
     apply_docs(
-        n, aliased(b.dst, b.src, "fold"),
+        n, aliased(b.dst, b.src, "fold", b.sorted_states),
         [&](size_t d, DocPlan& p) {
             p.a.plan(b.dk, b.da, b.dc, b.dit, b.dfirst[d], b.dfirst[d + 1] - b.dfirst[d], co.keys, co.actors,
                      co.counters, co.offsets[d], co.counts[d], b.sk, b.sit, b.sfirst.data(), b.src_beg[d],

@@ -205,6 +205,23 @@ def test_fold_wave_path_random(eng, mode):
     assert_same(eng.fold(mode, dst, srcs), want, dst.n_docs, R)
 
 
+@pytest.mark.parametrize("universe,max_src", [(16, 4), (40, 15), (64, 15), (64, 16), (65, 8)])
+@pytest.mark.parametrize("mode", [CRDT_FOLD_AWSET, CRDT_FOLD_DELTA])
+def test_fold_dense_key_spans(eng, mode, universe, max_src):
+    """Documents whose keys span few ids -- the per-slot AWSet walk (span < 64,
+    <= 15 sources) and the counting sort (span < 256) -- at and around their
+    limits (64 ids, 15/16 sources, 65 ids fall back), with entries that cover
+    or not the clocks so that adds, skips, removals and src-wins all occur."""
+    rng = random.Random(universe * 100 + max_src + mode)
+    R = 4
+    dst, srcs = fold_case(rng, 4000, R, lambda: rng.randint(0, min(universe, 60)), lambda: rng.randint(0, max_src),
+                          lambda: rng.randint(0, min(universe, 12)), lambda: rng.randint(0, 3), universe, 9,
+                          mode == CRDT_FOLD_DELTA)
+    rc, want = oracle.fold(mode, dst, srcs)
+    assert rc == 0
+    assert_same(eng.fold(mode, dst, srcs), want, dst.n_docs, R)
+
+
 @pytest.mark.parametrize("mode", [CRDT_FOLD_AWSET, CRDT_FOLD_DELTA])
 def test_fold_block_path_and_overflow(eng, mode):
     """Docs that start above CAP, grow above CAP mid-fold, or carry > 64 entries/tombstones per source."""
