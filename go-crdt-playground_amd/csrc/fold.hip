@@ -81,11 +81,13 @@ struct FoldSmem {
     uint32_t ta[NCAP];        // tuple actors
     uint32_t soff[MCAP + 1];  // source entry ranges, relative to the first source
     uint32_t sact[MCAP];      // source actors (AWSetDelta.Actor)
-    uint16_t stag[NCAP];      // kept tuples' tags
-    uint8_t anye[MCAP];       // step j has a changed entry
-    uint8_t anyt[MCAP];       // step j has an effective tombstone
+    // 8-byte aligned: the AWSet walk keeps 64-bit slot masks here, updated
+    // with 64-bit LDS atomics, which fault on a misaligned address
+    alignas(8) uint16_t stag[NCAP];  // kept tuples' tags
+    uint8_t anye[MCAP];              // step j has a changed entry
+    uint8_t anyt[MCAP];              // step j has an effective tombstone
     alignas(4) uint8_t smark[NCAP];  // s + 1 where source s's entries / tombstones end (step of a tuple)
-    uint16_t dbase[256];             // dense_sort: first sorted position of each key slot
+    alignas(8) uint16_t dbase[256];  // dense_sort: first sorted position of each key slot (64-bit stores)
 };
 
 // Tuple tag: bits 15..8 = 0 for a document entry, (j+1)*2 for an entry of
