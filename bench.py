@@ -612,6 +612,57 @@ def run_config(config, n, args, ctx, steps, warmup, repeats, cpu, box=None):
     return res
 
 
+def ingest_sort_leg(eng, dev, stream, n, seed, reps=10):
+    """The hand-written ingest sort (crdt_awset_sort_async, csrc/sort.hip) on
+    one replica of the config-2 pair with every document's live entries put in
+    a random order first -- the order a producer packing Go maps in iteration
+    order hands over (awset.go:55-59).  Timed with HIP events on the launch
+    stream; checked against the generator's sorted replica."""
+    import torch
+
+    from crdtgpu.batch import AWSetBatch, OutBuffers
+
+    R, E = 2, 64
+    A = OutBuffers(n, R, n * E, device=dev)
+    B = OutBuffers(n, R, n * E, device=dev)
+    eng.gen_pair_async(seed, n, A, B, stream=stream)
+    torch.cuda.synchronize()
+    del B
+    offs = A.offsets.to(torch.int64)
+    if not bool((offs[:n] == torch.arange(n, device=dev) * E).all()):
+        return {"error": "generator layout is not 64 slots per doc"}
+    cnt = A.counts.to(torch.int64).view(n, 1)
+    pos = torch.arange(E, device=dev).view(1, E)
+    g = torch.Generator(device=dev)
+    g.manual_seed(seed)
+    # live entries first in a random order, the slack after them
+    perm = torch.argsort(torch.rand(n, E, device=dev, generator=g) + (pos >= cnt).to(torch.float32) * 2, dim=1)
+    perm = (perm + torch.arange(n, device=dev).view(n, 1) * E).view(-1)
+    keys, acts, ctrs = A.keys[perm].contiguous(), A.actors[perm].contiguous(), A.counters[perm].contiguous()
+    inb = AWSetBatch(R, A.offsets, keys, acts, ctrs, A.vv, counts=A.counts)
+    out = OutBuffers(n, R, n * E, device=dev)
+    eng.sort_async(inb, n * E, out, stream=stream)
+    torch.cuda.synchronize()
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    with torch.cuda.stream(stream):
+        ev[0].record(stream)
+        for _ in range(reps):
+            eng.sort_async(inb, n * E, out, stream=stream)
+        ev[1].record(stream)
+    torch.cuda.synchronize()
+    ms = ev[0].elapsed_time(ev[1]) / reps
+    live = (pos < cnt).view(-1)
+    exact = bool(torch.equal(out.keys[live], A.keys[live]) and torch.equal(out.actors[live], A.actors[live])
+                 and torch.equal(out.counters[live], A.counters[live]) and torch.equal(out.counts, A.counts))
+    n_live = int(A.counts.to(torch.int64).sum())
+    nbytes = n_live * 40 + n * (R * 16 + 16)  # entries read + written (20 B each way), VVs, bounds and counts
+    return {"docs": n, "entries": n_live, "ms": ms, "docs_per_s": n / (ms * 1e-3), "entries_per_s": n_live / (ms * 1e-3),
+            "achieved_gbs": nbytes / (ms * 1e-3) / 1e9, "exact": exact,
+            "what": "crdt_awset_sort_async on one config-2 replica (64 slots/doc) with each doc's live entries "
+                    "shuffled on the device first; %d launches timed with HIP events, result equal to the "
+                    "generator's sorted replica" % reps}
+
+
 def boundary_cost(n_docs):
     """the host side of the drop-in, phase by phase, through
     the C++ host mirror's ExchangeBatch (tests/cpp/boundary_bench.cpp):
@@ -659,6 +710,7 @@ def main():
     ap.add_argument("--no-graph", action="store_true", help="launch eagerly instead of replaying a captured HIP graph")
     ap.add_argument("--no-boundary", action="store_true", help="skip the host boundary-cost leg")
     ap.add_argument("--no-box-probe", action="store_true", help="skip the box bandwidth probes")
+    ap.add_argument("--no-sort", action="store_true", help="skip the ingest-sort leg")
     ap.add_argument("--boundary-docs", type=int, default=65536)
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
     args = ap.parse_args()
@@ -725,8 +777,18 @@ def main():
         for c in legs:
             result["legs"]["config%d" % c] = run_config(c, DEFAULT_DOCS[c], args, ctx, args.leg_steps,
                                                         args.leg_warmup, 1, not args.no_cpu_baseline, box)
+    if rank == 0 and world == 1 and not args.no_sort:
+        result["ingest_sort"] = ingest_sort_leg(eng, dev, stream, DEFAULT_DOCS[2], args.seed)
     if rank == 0 and world == 1 and not args.no_boundary:
         result["boundary"] = boundary_cost(args.boundary_docs)
+        if not args.no_sort:
+            bs = ingest_sort_leg(eng, dev, stream, args.boundary_docs, args.seed)
+            if "ms" in bs:
+                # both replicas of the boundary batch, were they packed in map order
+                result["boundary"]["sort_s"] = 2 * bs["ms"] * 1e-3
+                result["boundary"]["sort_what"] = ("device ingest sort of both replicas of the boundary batch packed "
+                                                   "in map iteration order (not on the mirror's path, which places "
+                                                   "entries by id directly while packing)")
     if rank == 0:
         print(json.dumps(result), flush=True)
     eng.close()

@@ -216,42 +216,36 @@ __device__ __forceinline__ bool dense_sort(Smem& m, uint64_t (&k)[EPL], uint32_t
 }
 
 // The AWSet fold (every step a full (*AWSet).Merge, awset.go:107-161)
-// replayed per key slot when the document's keys span fewer than 64 ids and it
-// has at most 15 sources: lane s owns key kmin + s and walks the steps in
-// order, the key's state (present, dot) in registers -- the reference's rule
-// one key at a time:
+// resolved per key slot when the document's keys span fewer than 64 ids and it
+// has at most 15 sources: lane s owns key kmin + s.  The reference's rule, one
+// key at a time, over the steps in order:
 //   key in source j:  present -> dot := the source's dot (awset.go:123-129,142)
 //                     absent  -> added iff !HasDot(V_j, dot) (:133-140)
 //   not in source j:  present -> removed iff HasDot(svv_j, dot) (:146-158)
 // V_j is the clock before step j (the schedule's prefix max: an AWSet fold has
-// no no-op steps).  HasDot is evaluated exactly where Go evaluates it, so
-// actor == R flags exactly the reference's panics.  Tables alias tk and stag
-// (dead once the keys are in registers): mask[row] = the slots present in a
-// row (row 0 the document, row j + 1 source j), idx[row * 64 + slot] = the
-// tuple.  Survivors come out in slot = key order, one store round.  Returns
-// false (nothing changed) when the document does not qualify.
+// no no-op steps).  Rows: row 0 the document, row j + 1 source j.  A key's
+// tuples, in row order, each hold the current dot from their row until the
+// key's next row; so, per tuple t at row r:
+//   add_t  = t is the document's, or !HasDot(V_{r-1}, dot_t)
+//   drop_t = HasDot(svv_j, dot_t) for some step j in [r, next row - 1)
+// and the key survives iff some tuple has add set and no tuple from the last
+// such row on has drop set (an add makes the key present whatever it was
+// before; a drop removes it while present; a tuple without add keeps the
+// state it finds).  The survivor's dot is its last tuple's.  Each tuple's
+// bits are independent, so every check is one lane-parallel LDS read instead
+// of a step-by-step chain; the per-slot words (rows, add, drop, last tuple)
+// live in tk, dead once the keys are in registers.  Go evaluates HasDot only
+// where the step-by-step walk does, and panics at actor == len(VV): a document
+// holding such an actor takes that walk instead (dense_awset_walk_seq), so
+// the reference's panics are flagged exactly.  Survivors come out in slot =
+// key order, one store round.  Returns false (nothing changed) when the
+// document does not qualify.
 template <int NCH, class Smem>
-__device__ __forceinline__ bool dense_awset_walk(Smem& m, const uint64_t (&key)[NCH], const uint32_t (&step)[NCH],
-                                                 uint32_t N, uint32_t n, uint32_t ms, uint32_t R, uint32_t lane,
-                                                 uint64_t lt, Emit<NCH>& e, uint32_t& U, uint32_t& err) {
-    static_assert(sizeof(m.tk) >= 16 * 64 && sizeof(m.stag) >= 16 * 8, "dense_awset_walk: table space");
-    if (N == 0 || ms > 15) return false;
-    const uint64_t b = readlane64(key[0], 0);  // element 0 is valid
-    bool bad = false;
-    uint32_t lo = ~0u, hi = 0u;
-#pragma unroll
-    for (int c = 0; c < NCH; ++c) {
-        const bool valid = c * 64u + lane < N;
-        const uint64_t d = key[c] - b + 0x80000000ull;
-        bad |= valid && (d >> 32) != 0;
-        lo = valid ? min(lo, (uint32_t)d) : lo;
-        hi = valid ? max(hi, (uint32_t)d) : hi;
-    }
-    if (ballot(bad)) return false;
-    lo = wave_minmax<false>(lo);
-    hi = wave_minmax<true>(hi);
-    if (hi - lo >= 64u) return false;
-    const uint64_t kb = b - 0x80000000ull + lo;  // key of slot 0
+__device__ __forceinline__ void dense_awset_walk_seq(Smem& m, const uint64_t (&key)[NCH], const uint32_t (&step)[NCH],
+                                                     uint64_t kb, uint32_t N, uint32_t n, uint32_t ms, uint32_t R,
+                                                     uint32_t lane, bool& P, uint32_t& da, uint64_t& dc,
+                                                     uint32_t& err) {
+    // mask[row] = the slots present in a row, idx[row * 64 + slot] = the tuple
     uint64_t* mask = reinterpret_cast<uint64_t*>(m.stag);
     uint8_t* idx = reinterpret_cast<uint8_t*>(m.tk);
     if (lane <= ms) mask[lane] = 0ull;
@@ -267,9 +261,9 @@ __device__ __forceinline__ bool dense_awset_walk(Smem& m, const uint64_t (&key)[
         }
     }
     wave_sync();
-    bool P = (mask[0] >> lane) & 1ull;
-    uint32_t da = 0;
-    uint64_t dc = 0;
+    P = (mask[0] >> lane) & 1ull;
+    da = 0;
+    dc = 0;
     if (P) {
         const uint32_t t = idx[lane];
         da = m.ta[t];
@@ -294,6 +288,93 @@ __device__ __forceinline__ bool dense_awset_walk(Smem& m, const uint64_t (&key)[
         }
     }
     if (perr) err |= kErrActorRange;
+}
+
+template <int NCH, class Smem>
+__device__ __forceinline__ bool dense_awset_walk(Smem& m, const uint64_t (&key)[NCH], const uint32_t (&step)[NCH],
+                                                 uint32_t N, uint32_t n, uint32_t ms, uint32_t R, uint32_t lane,
+                                                 uint64_t lt, Emit<NCH>& e, uint32_t& U, uint32_t& err) {
+    static_assert(sizeof(m.tk) >= 16 * 64 && sizeof(m.stag) >= 16 * 8, "dense_awset_walk: table space");
+    if (N == 0 || ms > 15) return false;
+    const uint64_t b = readlane64(key[0], 0);  // element 0 is valid
+    bool bad = false;
+    uint32_t lo = ~0u, hi = 0u;
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+        const bool valid = c * 64u + lane < N;
+        const uint64_t d = key[c] - b + 0x80000000ull;
+        bad |= valid && (d >> 32) != 0;
+        lo = valid ? min(lo, (uint32_t)d) : lo;
+        hi = valid ? max(hi, (uint32_t)d) : hi;
+    }
+    if (ballot(bad)) return false;
+    lo = wave_minmax<false>(lo);
+    hi = wave_minmax<true>(hi);
+    if (hi - lo >= 64u) return false;
+    const uint64_t kb = b - 0x80000000ull + lo;  // key of slot 0
+    uint32_t a[NCH], sl[NCH], row[NCH];
+    uint64_t cc[NCH];
+    bool anyR = false;
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+        const uint32_t i = c * 64u + lane;
+        const bool valid = i < N;
+        a[c] = m.ta[valid ? i : 0u];
+        cc[c] = m.tc[valid ? i : 0u];
+        sl[c] = (uint32_t)(key[c] - kb) & 63u;
+        row[c] = i < n ? 0u : (step[c] & 63u) + 1u;
+        anyR |= valid && a[c] == R;
+    }
+    bool P;
+    uint32_t da;
+    uint64_t dc;
+    if (ballot(anyR)) {
+        dense_awset_walk_seq<NCH>(m, key, step, kb, N, n, ms, R, lane, P, da, dc, err);
+    } else {
+        uint32_t* rows = reinterpret_cast<uint32_t*>(m.tk);  // [64] rows holding the slot
+        uint32_t* addw = rows + 64;                          // [64] rows with add set
+        uint32_t* dropw = rows + 128;                        // [64] rows with drop set
+        uint8_t* last = reinterpret_cast<uint8_t*>(rows + 192);  // [64] the slot's last tuple
+        rows[lane] = 0u;
+        addw[lane] = 0u;
+        dropw[lane] = 0u;
+        wave_sync();
+#pragma unroll
+        for (int c = 0; c < NCH; ++c)
+            if (c * 64u + lane < N) atomicOr(&rows[sl[c]], 1u << row[c]);
+        wave_sync();
+#pragma unroll
+        for (int c = 0; c < NCH; ++c) {
+            const uint32_t i = c * 64u + lane;
+            if (i < N) {
+                const uint32_t r = row[c], above = rows[sl[c]] >> (r + 1u);
+                const uint32_t nr = above ? r + (uint32_t)__ffs(above) : ms + 1u;  // the key's next row
+                const bool cov = a[c] < R;  // actor > R: HasDot false (actor == R: the step walk)
+                const bool add = r == 0u || !(cov && m.vs[(r - 1u) * R + (cov ? a[c] : 0u)] >= cc[c]);
+                bool drop = false;
+                for (uint32_t j = r; j + 1u < nr; j += 4u) {  // four independent clock reads per round
+#pragma unroll
+                    for (uint32_t u = 0; u < 4u; ++u) {
+                        const bool in = cov && j + u + 1u < nr;
+                        drop |= in && m.svv[in ? (j + u) * R + a[c] : 0u] >= cc[c];
+                    }
+                }
+                if (add) atomicOr(&addw[sl[c]], 1u << r);
+                if (drop) atomicOr(&dropw[sl[c]], 1u << r);
+                if (!above) last[sl[c]] = (uint8_t)i;
+            }
+        }
+        wave_sync();
+        const uint32_t aw = addw[lane], dw = dropw[lane];
+        P = aw != 0u && (dw >> (31u - (uint32_t)__clz(aw))) == 0u;
+        da = 0;
+        dc = 0;
+        if (P) {
+            const uint32_t t = last[lane];
+            da = m.ta[t];
+            dc = m.tc[t];
+        }
+    }
     const uint64_t pm = ballot(P);
     U = popc(pm);
     e.k[0] = kb + lane;

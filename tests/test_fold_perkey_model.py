@@ -279,3 +279,64 @@ def test_step_of_tuple_marks(seed):
         for s, k in enumerate(tomb):
             want += [s] * k
         assert kernel_steps(n, ent, tomb) == want
+
+
+def slot_chain_fold(ents, vv0, chain):
+    """fold.hip dense_awset_walk's lane-parallel rule for the AWSet fold
+    (every step a full merge): per tuple t at row r (0 = the document, j + 1 =
+    source j), add_t = document tuple or !HasDot(V_{r-1}, dot_t); drop_t =
+    HasDot(svv_j, dot_t) for a step j in [r, the key's next row - 1).  The key
+    survives iff some tuple has add and none from the last such row on has
+    drop; the dot is the last tuple's.  Documents with actor == R take the
+    step walk in the kernel (exact panics), so they are not modelled here."""
+    R = len(vv0)
+    V = list(vv0)
+    Vs = []
+    for _, svv, _, _ in chain:
+        Vs.append(list(V))
+        V = [max(x, y) for x, y in zip(V, svv)]
+    rows = {}
+    for k, a, c in ents:
+        rows.setdefault(k, []).append((0, a, c))
+    for j, (_, _, e, _) in enumerate(chain):
+        for k, a, c in e:
+            rows.setdefault(k, []).append((j + 1, a, c))
+    ms = len(chain)
+    out = []
+    for k in sorted(rows):
+        tl = rows[k]
+        addw = dropw = 0
+        for x, (r, a, c) in enumerate(tl):
+            nr = tl[x + 1][0] if x + 1 < len(tl) else ms + 1
+            cov = a < R
+            add = r == 0 or not (cov and Vs[r - 1][a] >= c)
+            drop = cov and any(chain[j][1][a] >= c for j in range(r, nr - 1))
+            addw |= add << r
+            dropw |= drop << r
+        if addw and (dropw >> (addw.bit_length() - 1)) == 0:
+            out.append((k, tl[-1][1], tl[-1][2]))
+    return out, V
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_slot_chain_rule_matches_oracle(seed):
+    rng = random.Random(7000 + seed)
+    checked = 0
+    for _ in range(300):
+        R = rng.choice([1, 2, 3, 5])
+        ents, vv0, chain = rand_doc(rng, R, CRDT_FOLD_AWSET)
+        chain = chain[:15]
+        acts = [a for _, a, _ in ents] + [a for _, _, e, _ in chain for _, a, _ in e]
+        if R in acts:
+            continue  # the kernel's step walk (exact panics)
+        dst = AWSetBatch.from_docs(R, [(ents, vv0)])
+        srcs = SrcBatch.from_lists(R, [[(a, v, e, t) for a, v, e, t in chain]])
+        rc, want = oracle.fold(CRDT_FOLD_AWSET, dst, srcs)
+        assert rc == 0
+        got, vv = slot_chain_fold(ents, vv0, chain)
+        c, o = int(want.counts[0]), int(want.offsets[0])
+        exp = list(zip(want.keys[o:o + c].tolist(), want.actors[o:o + c].tolist(), want.counters[o:o + c].tolist()))
+        assert got == exp, (ents, vv0, chain)
+        assert vv == want.vv[:R].tolist()
+        checked += 1
+    assert checked > 150

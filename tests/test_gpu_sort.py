@@ -60,6 +60,47 @@ def test_sort_random_docs(eng, slack):
         assert got.vv[d * R:(d + 1) * R].tolist() == b.doc(d)[1]
 
 
+@pytest.mark.parametrize("universe", [600, 30_000, 10 ** 15, 2 ** 64])
+def test_sort_key_widths_and_run_edges(eng, universe):
+    """Every compare width of the in-register sort (keys spanning < 2^15 ids:
+    32-bit packed; < 2^47: 64-bit packed; wider, up to the full u64 range:
+    80-bit) and the run edges of both paths (64/128/256 in registers, 257+
+    through the merge-path passes, 1 to 4 passes)."""
+    rng = random.Random(universe % 1000 + 7)
+    nrng = np.random.default_rng(universe % 1000 + 7)
+    R = 2
+    sizes = [0, 1, 63, 64, 65, 127, 128, 129, 255, 256, 257, 511, 512, 513, 1024, 1025, 2049, 4100]
+    def state(n):
+        if universe < 2 ** 62:
+            return random_state(rng, R, min(n, universe), universe, 50)
+        ks = {0, 2 ** 64 - 1} if n >= 2 else set()  # both ends of the key range
+        while len(ks) < n:
+            ks.add(rng.getrandbits(64))
+        return [(k, rng.randint(0, R - 1), rng.randint(1, 50)) for k in sorted(ks)], [rng.randint(0, 50)] * R
+
+    docs = [state(n) for n in sizes for _ in range(3)]
+    b = batch_of(R, docs, slack=1)
+    got = eng.sort(shuffled(b, nrng))
+    for d in range(b.n_docs):
+        o, n = int(got.offsets[d]), int(got.counts[d])
+        assert n == b.live(d)
+        e = list(zip(got.keys[o:o + n].tolist(), got.actors[o:o + n].tolist(), got.counters[o:o + n].tolist()))
+        assert e == b.doc(d)[0], (d, n)
+
+
+@pytest.mark.parametrize("n", [40, 200, 3000])
+def test_sort_duplicate_in_each_path(eng, n):
+    """A repeated key is found by the register path and the merge-path passes."""
+    nrng = np.random.default_rng(n)
+    keys = nrng.choice(np.arange(10 ** 6, dtype=np.uint64), n, replace=False)
+    keys[n // 2] = keys[n // 3]
+    b = AWSetBatch(2, np.array([0, n], np.uint32), keys, np.zeros(n, np.uint32), np.ones(n, np.uint64),
+                   np.zeros(2, np.uint64))
+    with pytest.raises(crdtgpu.CrdtError) as ei:
+        eng.sort(b)
+    assert ei.value.code == crdtgpu.CRDT_E_DUP_KEY
+
+
 def test_sort_large_doc_and_duplicates(eng):
     nrng = np.random.default_rng(2)
     n = 100_000
