@@ -354,7 +354,7 @@ __global__ __launch_bounds__(256) void tomb_gc_kernel(TombView tb, uint32_t n_do
             const bool keep = v && !covered;
             const uint64_t m = ballot(keep);
             if (keep) {
-                const uint32_t pos = kept + popc(m & lt);
+                const uint32_t pos = kept + below(m);
                 out.keys[o + pos] = k;
                 out.actors[o + pos] = a;
                 out.counters[o + pos] = c;

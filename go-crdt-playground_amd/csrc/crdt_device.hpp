@@ -152,6 +152,12 @@ __device__ __forceinline__ uint64_t ballot(bool p) { return __ballot(p); }
 __device__ __forceinline__ uint32_t popc(uint64_t m) { return (uint32_t)__popcll(m); }
 
 // Bits [0, n) set, n in [0, 64].
+// Set bits of m below this lane (popc(m & low_mask(lane))), by mbcnt: two VALU
+// ops and no lane-mask register.
+__device__ __forceinline__ uint32_t below(uint64_t m) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
 __device__ __forceinline__ uint64_t low_mask(uint32_t n) { return n >= 64 ? ~0ull : ((1ull << n) - 1ull); }
 
 // Number of elements of the sorted a[0..n) strictly less than key; n <= 2^LOG.

@@ -57,13 +57,16 @@ namespace crdt {
 #ifndef CRDT_FOLD_DELTA_WPE
 #define CRDT_FOLD_DELTA_WPE 3  // probe builds may override (tools/fold_probe.hip)
 #endif
+#ifndef CRDT_FOLD_AWSET_WPE
+#define CRDT_FOLD_AWSET_WPE 5  // 96 VGPRs: 3 loop-invariant values spill (measured 11 % faster than 4)
+#endif
 // NCH: 64-tuple chunks a document may fill on this path (AWSet folds: 128
 // tuples -- fewer registers for the prefetch and the walk, so the kernel fits
 // 128 VGPRs with no spills; larger documents take the block kernel).  VCH:
 // 64-word chunks of source clocks.
 template <bool DELTA>
 struct FoldShape {
-    static constexpr int WPE = DELTA ? CRDT_FOLD_DELTA_WPE : 4;
+    static constexpr int WPE = DELTA ? CRDT_FOLD_DELTA_WPE : CRDT_FOLD_AWSET_WPE;
     static constexpr int NCH = DELTA ? 4 : 2;
     static constexpr int VCH = DELTA ? 4 : 2;
     static constexpr int VCAP = (DELTA && CRDT_FOLD_DELTA_WPE < 4) ? 256 : (DELTA ? 224 : 128);
@@ -83,7 +86,7 @@ struct FoldSmem {
     uint32_t sact[MCAP];      // source actors (AWSetDelta.Actor)
     // 8-byte aligned: the AWSet walk keeps 64-bit slot masks here, updated
     // with 64-bit LDS atomics, which fault on a misaligned address
-    alignas(8) uint16_t stag[NCAP];  // kept tuples' tags
+    alignas(16) uint16_t stag[NCAP];  // kept tuples' tags
     uint8_t anye[MCAP];              // step j has a changed entry
     uint8_t anyt[MCAP];              // step j has an effective tombstone
     alignas(4) uint8_t smark[NCAP];  // s + 1 where source s's entries / tombstones end (step of a tuple)
@@ -380,7 +383,7 @@ __device__ __forceinline__ bool dense_awset_walk(Smem& m, const uint64_t (&key)[
     e.k[0] = kb + lane;
     e.a[0] = da;
     e.c[0] = dc;
-    e.off[0] = P ? popc(pm & lt) : kOOB;
+    e.off[0] = P ? below(pm) : kOOB;
 #pragma unroll
     for (int q = 1; q < NCH; ++q) {
         e.k[q] = 0;
@@ -388,6 +391,128 @@ __device__ __forceinline__ bool dense_awset_walk(Smem& m, const uint64_t (&key)[
         e.c[q] = 0;
         e.off[q] = kOOB;
     }
+    return true;
+}
+
+// The delta fold's kept tuples resolved per key slot, as dense_awset_walk does
+// for the AWSet fold, when the keys span fewer than 256 ids (4 slots per lane:
+// slot q * 64 + lane) and there are at most 15 sources.  The rule of
+// sort_resolve, slot-wise: times 0 (document), 2j + 1 (entry of step j),
+// 2j + 2 (tombstone of step j); per kept tuple t
+//   document entry        add;  drop = a full step of its gap covers its dot
+//   entry, full step j    add iff !HasDot(V_j, dot);  drop as above
+//   changed entry, delta  add;  drop as above
+//   effective tombstone   drop iff !HasDot(V_j, dot) (awset-delta_test.go:149-164)
+// where an entry's gap is the full steps after it up to the key's next entry
+// (tombstones do not move the dot; a removal there precedes any later add, so
+// attributing it to the entry's time is exact).  The key survives iff some
+// tuple adds and none from the last add's time on drops; its dot is the last
+// entry's.  Per-slot words: entry times and add times in tk, drop times and the
+// last entry in stag..dbase (all dead by now).  A document with a kept tuple of
+// actor == len(VV) is left to the sort path (exact panics).
+template <class Smem>
+__device__ __forceinline__ bool dense_delta_walk(Smem& m, const uint64_t (&key)[4], const uint32_t (&step)[4],
+                                                 const bool (&isE)[4], const bool (&isT)[4], uint32_t flag,
+                                                 uint64_t full_mask, uint64_t noop_mask, uint32_t N, uint32_t n,
+                                                 uint32_t ms, uint32_t R, uint32_t lane, uint64_t lt, Emit<4>& e,
+                                                 uint32_t& U STAMP_PARAM) {
+    static_assert(sizeof(m.tk) >= 2 * 256 * 4, "dense_delta_walk: entry/add words");
+    static_assert(offsetof(Smem, dbase) + sizeof(m.dbase) - offsetof(Smem, stag) >= 256 * 5,
+                  "dense_delta_walk: drop words + last entry");
+    if (N == 0 || ms > 15) return false;
+    bool kept[4];
+    uint32_t a[4];
+    bool anyR = false, bad = false;
+    const uint64_t b = readlane64(key[0], 0);  // element 0 is valid
+    uint32_t lo = ~0u, hi = 0u;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        const uint32_t i = c * 64u + lane;
+        const uint32_t j = step[c] & 63u;
+        const bool fj = (full_mask >> j) & 1ull, nj = (noop_mask >> j) & 1ull, f = (flag >> c) & 1u;
+        kept[c] = i < N && ((i < n) || (isE[c] && !nj && (fj || f)) || (isT[c] && !nj && !fj && f));
+        a[c] = m.ta[i < N ? i : 0u];
+        anyR |= kept[c] && a[c] == R;
+        const uint64_t d = key[c] - b + 0x80000000ull;
+        bad |= kept[c] && (d >> 32) != 0;
+        lo = kept[c] ? min(lo, (uint32_t)d) : lo;
+        hi = kept[c] ? max(hi, (uint32_t)d) : hi;
+    }
+    if (ballot(anyR || bad)) return false;
+    lo = wave_minmax<false>(lo);
+    hi = wave_minmax<true>(hi);
+    if (lo > hi || hi - lo >= 256u) return false;  // lo > hi: nothing kept
+    const uint64_t kb = b - 0x80000000ull + lo;   // key of slot 0
+    uint32_t* erows = reinterpret_cast<uint32_t*>(m.tk);  // [256] entry times of the slot
+    uint32_t* addw = erows + 256;                          // [256] add times
+    uint32_t* dropw = reinterpret_cast<uint32_t*>(m.stag);  // [256] drop times
+    uint8_t* last = reinterpret_cast<uint8_t*>(dropw + 256);  // [256] the slot's last entry
+    STAMP(7)
+    const uint4 z4 = make_uint4(0u, 0u, 0u, 0u);
+    reinterpret_cast<uint4*>(erows)[lane] = z4;
+    reinterpret_cast<uint4*>(addw)[lane] = z4;
+    reinterpret_cast<uint4*>(dropw)[lane] = z4;
+    wave_sync();
+    uint32_t tm[4], sl[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        const uint32_t i = c * 64u + lane;
+        sl[c] = (uint32_t)(key[c] - kb) & 255u;
+        tm[c] = i < n ? 0u : (step[c] & 63u) * 2u + (isT[c] ? 2u : 1u);
+        if (kept[c] && !isT[c]) atomicOr(&erows[sl[c]], 1u << tm[c]);
+    }
+    wave_sync();
+    STAMP(8)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        if (!kept[c]) continue;
+        const uint32_t i = c * 64u + lane;
+        const uint64_t cc = m.tc[i];
+        const bool cov = a[c] < R;  // actor > R: HasDot false
+        const uint32_t r = tm[c], j = (r - 1u) >> 1;  // j: the tuple's step (unused for the document)
+        if (isT[c]) {
+            if (!(cov && m.vs[j * R + (cov ? a[c] : 0u)] >= cc)) atomicOr(&dropw[sl[c]], 1u << r);
+            continue;
+        }
+        const uint32_t above = erows[sl[c]] >> (r + 1u);
+        const uint32_t jn = above ? (r + (uint32_t)__ffs(above) - 1u) >> 1 : ms;  // the key's next entry step
+        const uint32_t j0 = r == 0u ? 0u : j + 1u;
+        uint64_t gap = cov ? full_mask & low_mask(jn) & ~low_mask(j0) : 0ull;
+        bool drop = false;
+        while (gap) {  // full steps of the gap: HasDot(svv_g, dot) (awset.go:146-158)
+            const uint32_t g = (uint32_t)__ffsll((unsigned long long)gap) - 1u;
+            gap &= gap - 1ull;
+            drop |= m.svv[g * R + a[c]] >= cc;
+        }
+        const bool fj = r != 0u && ((full_mask >> j) & 1ull);
+        const bool add = !fj || !(cov && m.vs[j * R + (cov ? a[c] : 0u)] >= cc);
+        if (add) atomicOr(&addw[sl[c]], 1u << r);
+        if (drop) atomicOr(&dropw[sl[c]], 1u << r);
+        if (!above) last[sl[c]] = (uint8_t)i;
+    }
+    wave_sync();
+    STAMP(9)
+    uint32_t base = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const uint32_t s = q * 64u + lane;
+        const uint32_t aw = addw[s], dw = dropw[s];
+        const bool P = aw != 0u && (dw >> (31u - (uint32_t)__clz(aw))) == 0u;
+        uint32_t da = 0;
+        uint64_t dc = 0;
+        if (P) {
+            const uint32_t t = last[s];
+            da = m.ta[t];
+            dc = m.tc[t];
+        }
+        const uint64_t pm = ballot(P);
+        e.k[q] = kb + s;
+        e.a[q] = da;
+        e.c[q] = dc;
+        e.off[q] = P ? base + below(pm) : kOOB;
+        base += popc(pm);
+    }
+    U = base;
     return true;
 }
 
@@ -580,15 +705,17 @@ __global__ __launch_bounds__(kFoldWaves * 64) __attribute__((amdgpu_waves_per_eu
     auto meta = [&](uint32_t k) {
         DocMeta q;
         q.d = first + k;
+        // bounds of lanes k and k + 1 (lane cnt holds the run's end): only the
+        // base vectors stay live through the loop, not their differences
         q.doff = rl(mv_off, k);
-        q.slots = rl(slots_i, k);
+        q.slots = rl(mv_off, k + 1) - q.doff;
         q.n = rl(n_i, k);
         q.s0 = rl(mv_ds, k);
-        q.ms = rl(ms_i, k);
+        q.ms = rl(mv_ds, k + 1) - q.s0;
         q.e0 = rl(mv_eo, k);
-        q.E = rl(E_i, k);
+        q.E = rl(mv_eo, k + 1) - q.e0;
         q.t0 = rl(mv_to, k);
-        q.X = rl(X_i, k);
+        q.X = rl(mv_to, k + 1) - q.t0;
         q.N = q.n + q.E + q.X;
         q.big = (uint32_t)((bigm >> k) & 1ull);
         return q;
@@ -881,8 +1008,13 @@ __global__ __launch_bounds__(kFoldWaves * 64) __attribute__((amdgpu_waves_per_eu
                 wave_sync();
             }
             err |= perr;
+            STAMP(13)
             bool walked = false;
-            if constexpr (!DELTA) walked = dense_awset_walk<NCH>(m, key, step, N, n, ms, R, lane, lt, em, U, err);
+            if constexpr (!DELTA)
+                walked = dense_awset_walk<NCH>(m, key, step, N, n, ms, R, lane, lt, em, U, err);
+            else if constexpr (NCH == 4)
+                walked = dense_delta_walk(m, key, step, isE, isT, flag, full_mask, noop_mask, N, n, ms, R, lane, lt,
+                                          em, U STAMP_ARGS);
             if (!walked) {
             // keep + tag, compacted in place over m.tk (every read of m.tk is done)
             uint32_t Kc = 0;
@@ -898,7 +1030,7 @@ __global__ __launch_bounds__(kFoldWaves * 64) __attribute__((amdgpu_waves_per_eu
                     const uint32_t tag =
                         (isE[c] || isT[c]) ? ((((j + 1u) * 2u + (isT[c] ? 1u : 0u)) << 8) | i) : i;
                     const uint64_t km = ballot(kept);
-                    const uint32_t pos = Kc + popc(km & lt);
+                    const uint32_t pos = Kc + below(km);
                     if (kept) {
                         m.tk[pos] = key[c];
                         m.stag[pos] = (uint16_t)tag;

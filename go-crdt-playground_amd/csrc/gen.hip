@@ -51,11 +51,11 @@ __global__ __launch_bounds__(WAVES * 64) void gen_pair_kernel(uint64_t seed, uin
             const uint32_t n_ops1 = popc(ops1), n_pres1 = popc(pres1);  // n_pres1 == 40
             const uint64_t c0 = X == 0 ? 48ull : 0ull;                    // X's counter before its ops
             if (in_base && !del) {
-                const uint32_t idx = base + popc(pres1 & lt);
+                const uint32_t idx = base + below(pres1);
                 O.keys[idx] = ((uint64_t)d << 8) | u1;
                 if (re) {
                     O.actors[idx] = (uint32_t)X;
-                    O.counters[idx] = c0 + popc(ops1 & lt) + 1;
+                    O.counters[idx] = c0 + below(ops1) + 1;
                 } else {
                     O.actors[idx] = 0;
                     O.counters[idx] = u1 + 1;
@@ -356,16 +356,16 @@ __global__ __launch_bounds__(256) void gen_zipf_kernel(uint64_t seed, uint32_t n
             const uint64_t ma = ballot(in && !a_del), mb = ballot(in && !b_del);
             const uint64_t mra = ballot(b_del), mrb = ballot(a_del);  // A re-adds where B deletes
             if (in && !a_del) {
-                const uint32_t i = base + pa + popc(ma & lt);
+                const uint32_t i = base + pa + below(ma);
                 A.keys[i] = key;
                 A.actors[i] = 0;
-                A.counters[i] = b_del ? (uint64_t)size + ra + popc(mra & lt) + 1 : (uint64_t)u + 1;
+                A.counters[i] = b_del ? (uint64_t)size + ra + below(mra) + 1 : (uint64_t)u + 1;
             }
             if (in && !b_del) {
-                const uint32_t i = base + pb + popc(mb & lt);
+                const uint32_t i = base + pb + below(mb);
                 B.keys[i] = key;
                 B.actors[i] = a_del ? 1u : 0u;
-                B.counters[i] = a_del ? (uint64_t)rb + popc(mrb & lt) + 1 : (uint64_t)u + 1;
+                B.counters[i] = a_del ? (uint64_t)rb + below(mrb) + 1 : (uint64_t)u + 1;
             }
             pa += popc(ma);
             pb += popc(mb);

@@ -117,8 +117,8 @@ __device__ __forceinline__ void join_doc(JoinWaveSmem<WAVES>& sm, uint32_t w, co
     // awset.go:142: the src dot wins on a common key (lane j holds it).
     const uint32_t ma = __shfl(L.sa, (int)(j & 63));
     const uint64_t mc = __shfl(L.sc, (int)(j & 63));
-    const uint32_t dpos = popc(dm & lt) + popc(smk & low_mask(j));
-    const uint32_t spos = popc(smk & lt) + popc(dm & low_mask(i));
+    const uint32_t dpos = below(dm) + popc(smk & low_mask(j));
+    const uint32_t spos = below(smk) + popc(dm & low_mask(i));
     const uint32_t cap = dnn + snn;
     const rsrc_t ok = make_rsrc(out.keys + obase, cap * 8u);
     const rsrc_t oa = make_rsrc(out.actors + obase, cap * 4u);

@@ -251,7 +251,7 @@ __device__ __forceinline__ uint32_t lane_prefix_small(uint32_t c, uint64_t lt, u
 #pragma unroll
     for (int b = 0; b < 3; ++b) {
         const uint64_t mb = ballot((c >> b) & 1u);
-        pre += popc(mb & lt) << b;
+        pre += below(mb) << b;
         tot += popc(mb) << b;
     }
     return tot;

@@ -567,15 +567,28 @@ struct Plan {
             }
         }
     }
+    // A removed key's node is reused for an added key (extract, rename,
+    // reinsert): no free/allocate pair, and the map's size -- hence its bucket
+    // array -- does not change, so no rehash invalidates the iterators still
+    // to be used.  Only the adds beyond the removals allocate, after every
+    // iterator has been used.  (No reserve(): libstdc++'s rehash(n) also
+    // SHRINKS to n's bucket count, relinking every node.)
     void commit(AWSet& dst) {
-        for (auto it : erase) dst.entries.erase(it);
         for (auto& u : upd) u.first->second = u.second;
-        if (!ins.empty() || !ins_own.empty()) {
-            // no reserve(): libstdc++'s rehash(n) also SHRINKS to n's bucket
-            // count, relinking every node; inserts grow the table only when needed
-            for (auto& x : ins) dst.entries.emplace(*x.first, x.second);
-            for (auto& x : ins_own) dst.entries.emplace(std::move(x.first), x.second);
-        }
+        size_t k = 0;
+        auto put = [&](auto&& key, const Dot& dot) {
+            if (k < erase.size()) {
+                auto nh = dst.entries.extract(erase[k++]);
+                nh.key() = std::forward<decltype(key)>(key);
+                nh.mapped() = dot;
+                dst.entries.insert(std::move(nh));
+            } else {
+                dst.entries.emplace(std::forward<decltype(key)>(key), dot);
+            }
+        };
+        for (auto& x : ins) put(*x.first, x.second);
+        for (auto& x : ins_own) put(std::move(x.first), x.second);
+        for (; k < erase.size(); ++k) dst.entries.erase(erase[k]);
     }
 };
 
@@ -895,6 +908,7 @@ inline void MergeBatch(const std::vector<AWSet*>& dsts, const std::vector<const 
                        Engine& e = Engine::Default()) {
     using namespace detail;
     if (dsts.empty() && srcs.empty()) return;
+    LastStats() = BoundaryStats{};
     auto t0 = clk::now();
     Batch& b = join_batch(e, dsts, srcs, "MergeBatch");
     const crdt_awset_batch cd = pack(b, e, false), cs = src_view(b, e);
@@ -928,6 +942,7 @@ inline void ExchangeBatch(const std::vector<AWSet*>& as, const std::vector<AWSet
                           Engine& e = Engine::Default()) {
     using namespace detail;
     if (as.empty() && bs.empty()) return;
+    LastStats() = BoundaryStats{};
     auto t0 = clk::now();
     const auto t_call = t0;
     Batch& b = join_batch(e, as, bs, "ExchangeBatch");
@@ -971,6 +986,7 @@ inline void fold(int mode, const std::vector<AWSet*>& dsts, const std::vector<st
                  Engine& e) {
     if (dsts.size() != srcs.size()) throw Error(CRDT_E_INVALID, "fold: length mismatch");
     if (dsts.empty()) return;
+    LastStats() = BoundaryStats{};
     auto t0 = clk::now();
     Batch& b = e.batch();
     b.reset();

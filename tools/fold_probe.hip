@@ -90,7 +90,8 @@ int main(int argc, char** argv) {
     uint32_t status = 0;
     CK(hipMemcpy(&status, ws + 16, 4, hipMemcpyDeviceToHost));
     const char* names[16] = {"stage", "prefetch", "schedule", "classify", "noop+keep", "sort-group", "write",
-                             "sort", "elem-flags", "dot-scan+gaps", "step-of-tuple", "cmax", "meta-next", "", "", "doc-loop"};
+                             "sort|walk-span", "elem-flags|walk-rows", "dot-scan+gaps|walk-bits", "step-of-tuple", "cmax",
+                             "meta-next", "noop", "", "doc-loop"};
     double tot = 0;
     for (int i = 0; i < 16; ++i) tot += (double)st[i];
     printf("config %d: %u docs, %.3f ms per stamped launch, status %u\n", config, n, ms / reps, status);
