@@ -19,6 +19,10 @@ hipError_t launch_fold(int mode, const BatchView& dst, const SrcView& sb, const 
                        const Work& wk, uint32_t block_grid, hipStream_t stream);
 uint32_t tile_positions(uint32_t shape);
 hipError_t sort_storage(uint32_t n_docs, uint32_t n_slots, size_t* bytes);
+hipError_t launch_check_order(const uint32_t* off, const uint32_t* cnt, uint32_t n, const uint64_t* keys,
+                              uint32_t* status, uint32_t n_cu, hipStream_t stream);
+hipError_t launch_pack_out(const OutView& in, const uint32_t* poff, uint32_t n, const OutView& out, uint32_t n_cu,
+                           hipStream_t stream);
 hipError_t launch_sort(const BatchView& in, uint32_t n_slots, const OutView& out, void* temp, size_t temp_bytes,
                        uint32_t* ends, uint32_t* idx, uint32_t* status, uint32_t n_cu, hipStream_t stream);
 hipError_t launch_apply(const BatchView& st, const TombView& tb, const ApplyOps& ops, const OutView& out,
@@ -118,6 +122,7 @@ struct crdt_ctx {
     uint32_t join_docs_per_wave = 8;          // crdt_ctx_set_option("join_docs_per_wave")
     bool join_nt_stores = true;               // crdt_ctx_set_option("join_nt_stores")
     uint32_t probe_blocks_per_cu = 16;        // crdt_ctx_set_option("probe_blocks_per_cu")
+    bool pack_outputs = false;                // crdt_ctx_set_option("pack_batch_outputs")
     // staging for the *_batch host path
     DevBuf stage[32];
     hipStream_t stream = nullptr;
@@ -342,6 +347,10 @@ int crdt_ctx_set_option(crdt_ctx* ctx, const char* name, int64_t value) {
         ctx->join_tiles = value != 0;
         return CRDT_OK;
     }
+    if (!strcmp(name, "pack_batch_outputs")) {  // *_batch joins / exchanges / folds: live entries only, packed
+        ctx->pack_outputs = value != 0;
+        return CRDT_OK;
+    }
     if (!strcmp(name, "probe_blocks_per_cu")) {
         if (value < 1 || value > 64) return CRDT_E_INVALID;
         ctx->probe_blocks_per_cu = (uint32_t)value;
@@ -367,6 +376,7 @@ int crdt_ctx_sync(crdt_ctx* ctx, void* stream) {
         return CRDT_E_HIP;
     if (status) {
         if (hipMemset(ctx->ws.as<uint32_t>(64), 0, sizeof(uint32_t)) != hipSuccess) return CRDT_E_HIP;
+        if (status & kErrUnsorted) return CRDT_E_UNSORTED;
         if (status & kErrActorRange) return CRDT_E_ACTOR_RANGE;
         if (status & kErrWorkspace) return CRDT_E_WORKSPACE;
         if (status & kErrHint) return CRDT_E_INVALID;
@@ -659,7 +669,12 @@ int crdt_clock_probe(crdt_ctx* ctx, double* mhz) {
 
 /* ---------------- validation (host) ---------------- */
 
-int crdt_validate_batch(const crdt_awset_batch* b) {
+}  // extern "C"
+
+// Pointers, slot bounds, live counts and (keys = true) the key order.  The
+// *_batch calls check only the layout here (O(documents)) and the key order
+// on the device after the upload (pack.hip, check_order_kernel).
+static int validate_batch(const crdt_awset_batch* b, bool keys) {
     if (!b || !b->offsets || b->R == 0 || b->R > CRDT_MAX_R) return CRDT_E_INVALID;
     if (b->n_docs && (!b->vv || ((b->offsets[b->n_docs] > b->offsets[0]) && (!b->keys || !b->actors || !b->counters))))
         return CRDT_E_INVALID;
@@ -668,13 +683,14 @@ int crdt_validate_batch(const crdt_awset_batch* b) {
         if (e < o) return CRDT_E_INVALID;
         const uint32_t n = b->counts ? b->counts[d] : e - o;
         if (n > e - o) return CRDT_E_CAPACITY;
-        for (uint32_t i = o + 1; i < o + n; i++)
-            if (b->keys[i] <= b->keys[i - 1]) return CRDT_E_UNSORTED;
+        if (keys)
+            for (uint32_t i = o + 1; i < o + n; i++)
+                if (b->keys[i] <= b->keys[i - 1]) return CRDT_E_UNSORTED;
     }
     return CRDT_OK;
 }
 
-int crdt_validate_src_batch(const crdt_src_batch* s) {
+static int validate_src_batch(const crdt_src_batch* s, bool keys) {
     if (!src_ptrs_ok(s)) return CRDT_E_INVALID;
     const uint32_t ns = s->doc_srcs[s->n_docs];
     for (uint32_t d = 0; d < s->n_docs; d++)
@@ -683,17 +699,25 @@ int crdt_validate_src_batch(const crdt_src_batch* s) {
     for (uint32_t k = 0; k < ns; k++) {
         const uint32_t o = s->entry_off[k], e = s->entry_off[k + 1];
         if (e < o) return CRDT_E_INVALID;
-        for (uint32_t i = o + 1; i < e; i++)
-            if (s->keys[i] <= s->keys[i - 1]) return CRDT_E_UNSORTED;
+        if (keys)
+            for (uint32_t i = o + 1; i < e; i++)
+                if (s->keys[i] <= s->keys[i - 1]) return CRDT_E_UNSORTED;
         if (s->tomb_off) {
             const uint32_t to = s->tomb_off[k], te = s->tomb_off[k + 1];
             if (te < to) return CRDT_E_INVALID;
-            for (uint32_t i = to + 1; i < te; i++)
-                if (s->tkeys[i] <= s->tkeys[i - 1]) return CRDT_E_UNSORTED;
+            if (keys)
+                for (uint32_t i = to + 1; i < te; i++)
+                    if (s->tkeys[i] <= s->tkeys[i - 1]) return CRDT_E_UNSORTED;
         }
     }
     return CRDT_OK;
 }
+
+extern "C" {
+
+int crdt_validate_batch(const crdt_awset_batch* b) { return validate_batch(b, true); }
+
+int crdt_validate_src_batch(const crdt_src_batch* s) { return validate_src_batch(s, true); }
 
 int crdt_validate_tomb_batch(const crdt_tomb_batch* t, uint32_t n_docs) {
     if (!t || !t->offsets) return CRDT_E_INVALID;
@@ -776,6 +800,43 @@ int fetch_out(const crdt_awset_out* h, const crdt_awset_out& d, uint32_t n_docs,
     return rc;
 }
 
+// The key order of a staged batch (ranges off[r] .. + counts or off[r + 1]),
+// checked on the device; a violation reads back as CRDT_E_UNSORTED.
+int check_order(crdt_ctx* ctx, const uint32_t* off, const uint32_t* cnt, uint32_t n, const uint64_t* keys) {
+    return hip_err(launch_check_order(off, cnt, n, keys, ctx->ws.as<uint32_t>(64), (uint32_t)ctx->n_cu, ctx->stream));
+}
+
+// Download a merge output: at its capacity offsets, or (pack_batch_outputs)
+// only the live entries, gathered on the device at offsets = the prefix sums
+// of the counts, so PCIe moves live entries only.
+int fetch_merge_out(crdt_ctx* ctx, Stager& st, const crdt_awset_out* h, const crdt_awset_out& d, uint32_t n,
+                    uint32_t R, size_t slots) {
+    if (!ctx->pack_outputs) return fetch_out(h, d, n, R, slots, ctx->stream);
+    int rc = get(h->counts, d.counts, n, ctx->stream);
+    if (rc == CRDT_OK && hipStreamSynchronize(ctx->stream) != hipSuccess) rc = CRDT_E_HIP;
+    if (rc != CRDT_OK) return rc;
+    uint64_t tot = 0;
+    h->offsets[0] = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+        tot += h->counts[i];
+        if (tot > slots) {  // only after a failed merge (e.g. unsorted input): report that failure
+            const int sync = crdt_ctx_sync(ctx, ctx->stream);
+            return sync != CRDT_OK ? sync : CRDT_E_CAPACITY;
+        }
+        h->offsets[i + 1] = (uint32_t)tot;
+    }
+    const uint32_t* poff = st.put(h->offsets, (size_t)n + 1);
+    const crdt_awset_out p{nullptr, nullptr, st.room<uint64_t>(tot), st.room<uint32_t>(tot), st.room<uint64_t>(tot),
+                           nullptr};
+    if (st.rc != CRDT_OK) return st.rc;
+    rc = hip_err(launch_pack_out(view(&d), poff, n, view(&p), (uint32_t)ctx->n_cu, ctx->stream));
+    if (rc == CRDT_OK) rc = get(h->keys, p.keys, tot, ctx->stream);
+    if (rc == CRDT_OK) rc = get(h->actors, p.actors, tot, ctx->stream);
+    if (rc == CRDT_OK) rc = get(h->counters, p.counters, tot, ctx->stream);
+    if (rc == CRDT_OK) rc = get(h->vv, d.vv, (size_t)n * R, ctx->stream);
+    return rc;
+}
+
 }  // namespace
 
 extern "C" {
@@ -852,8 +913,8 @@ int crdt_awset_apply_batch(crdt_ctx* ctx, const crdt_awset_batch* state, const c
 int crdt_awset_join_batch(crdt_ctx* ctx, const crdt_awset_batch* dst, const crdt_awset_batch* src,
                           const crdt_awset_out* out) {
     if (!ctx || !out_ptrs_ok(out)) return CRDT_E_INVALID;
-    int rc = crdt_validate_batch(dst);
-    if (rc == CRDT_OK) rc = crdt_validate_batch(src);
+    int rc = validate_batch(dst, false);
+    if (rc == CRDT_OK) rc = validate_batch(src, false);
     if (rc != CRDT_OK) return rc;
     if (dst->n_docs != src->n_docs || dst->R != src->R) return CRDT_E_INVALID;
     if ((uint64_t)dst->offsets[dst->n_docs] + src->offsets[src->n_docs] >= (1ull << 32)) return CRDT_E_INVALID;
@@ -863,8 +924,10 @@ int crdt_awset_join_batch(crdt_ctx* ctx, const crdt_awset_batch* dst, const crdt
     const size_t slots = (size_t)dst->offsets[dst->n_docs] + src->offsets[src->n_docs];
     crdt_awset_out dout = stage_out(st, dst->n_docs, dst->R, slots);
     if (st.rc != CRDT_OK) return st.rc;
-    rc = crdt_awset_join_async(ctx, &dd, &ds, &dout, ctx->stream);
-    if (rc == CRDT_OK) rc = fetch_out(out, dout, dst->n_docs, dst->R, slots, ctx->stream);
+    rc = check_order(ctx, dd.offsets, dd.counts, dd.n_docs, dd.keys);
+    if (rc == CRDT_OK) rc = check_order(ctx, ds.offsets, ds.counts, ds.n_docs, ds.keys);
+    if (rc == CRDT_OK) rc = crdt_awset_join_async(ctx, &dd, &ds, &dout, ctx->stream);
+    if (rc == CRDT_OK) rc = fetch_merge_out(ctx, st, out, dout, dst->n_docs, dst->R, slots);
     const int sync = crdt_ctx_sync(ctx, ctx->stream);
     return rc != CRDT_OK ? rc : sync;
 }
@@ -872,8 +935,8 @@ int crdt_awset_join_batch(crdt_ctx* ctx, const crdt_awset_batch* dst, const crdt
 int crdt_awset_exchange_batch(crdt_ctx* ctx, const crdt_awset_batch* a, const crdt_awset_batch* b,
                               const crdt_awset_out* out_ab, const crdt_awset_out* out_ba) {
     if (!ctx || !out_ptrs_ok(out_ab) || !out_ptrs_ok(out_ba)) return CRDT_E_INVALID;
-    int rc = crdt_validate_batch(a);
-    if (rc == CRDT_OK) rc = crdt_validate_batch(b);
+    int rc = validate_batch(a, false);
+    if (rc == CRDT_OK) rc = validate_batch(b, false);
     if (rc != CRDT_OK) return rc;
     if (a->n_docs != b->n_docs || a->R != b->R) return CRDT_E_INVALID;
     if ((uint64_t)a->offsets[a->n_docs] + b->offsets[b->n_docs] >= (1ull << 32)) return CRDT_E_INVALID;
@@ -884,9 +947,11 @@ int crdt_awset_exchange_batch(crdt_ctx* ctx, const crdt_awset_batch* a, const cr
     crdt_awset_out o1 = stage_out(st, a->n_docs, a->R, slots);
     crdt_awset_out o2 = stage_out(st, a->n_docs, a->R, slots);
     if (st.rc != CRDT_OK) return st.rc;
-    rc = crdt_awset_exchange_async(ctx, &da, &db, &o1, &o2, ctx->stream);
-    if (rc == CRDT_OK) rc = fetch_out(out_ab, o1, a->n_docs, a->R, slots, ctx->stream);
-    if (rc == CRDT_OK) rc = fetch_out(out_ba, o2, a->n_docs, a->R, slots, ctx->stream);
+    rc = check_order(ctx, da.offsets, da.counts, da.n_docs, da.keys);
+    if (rc == CRDT_OK) rc = check_order(ctx, db.offsets, db.counts, db.n_docs, db.keys);
+    if (rc == CRDT_OK) rc = crdt_awset_exchange_async(ctx, &da, &db, &o1, &o2, ctx->stream);
+    if (rc == CRDT_OK) rc = fetch_merge_out(ctx, st, out_ab, o1, a->n_docs, a->R, slots);
+    if (rc == CRDT_OK) rc = fetch_merge_out(ctx, st, out_ba, o2, a->n_docs, a->R, slots);
     const int sync = crdt_ctx_sync(ctx, ctx->stream);
     return rc != CRDT_OK ? rc : sync;
 }
@@ -894,8 +959,8 @@ int crdt_awset_exchange_batch(crdt_ctx* ctx, const crdt_awset_batch* a, const cr
 int crdt_awset_fold_batch(crdt_ctx* ctx, int mode, const crdt_awset_batch* dst, const crdt_src_batch* srcs,
                           const crdt_awset_out* out) {
     if (!ctx || !out_ptrs_ok(out)) return CRDT_E_INVALID;
-    int rc = crdt_validate_batch(dst);
-    if (rc == CRDT_OK) rc = crdt_validate_src_batch(srcs);
+    int rc = validate_batch(dst, false);
+    if (rc == CRDT_OK) rc = validate_src_batch(srcs, false);
     if (rc != CRDT_OK) return rc;
     if (dst->n_docs != srcs->n_docs || dst->R != srcs->R) return CRDT_E_INVALID;
     const uint32_t ns = srcs->doc_srcs[srcs->n_docs];
@@ -923,8 +988,11 @@ int crdt_awset_fold_batch(crdt_ctx* ctx, int mode, const crdt_awset_batch* dst, 
     }
     crdt_awset_out dout = stage_out(st, dst->n_docs, dst->R, total);
     if (st.rc != CRDT_OK) return st.rc;
-    rc = crdt_awset_fold_async(ctx, mode, &dd, &ds, &dout, ctx->stream);
-    if (rc == CRDT_OK) rc = fetch_out(out, dout, dst->n_docs, dst->R, total, ctx->stream);
+    rc = check_order(ctx, dd.offsets, dd.counts, dd.n_docs, dd.keys);
+    if (rc == CRDT_OK) rc = check_order(ctx, ds.entry_off, nullptr, ns, ds.keys);
+    if (rc == CRDT_OK && srcs->tomb_off) rc = check_order(ctx, ds.tomb_off, nullptr, ns, ds.tkeys);
+    if (rc == CRDT_OK) rc = crdt_awset_fold_async(ctx, mode, &dd, &ds, &dout, ctx->stream);
+    if (rc == CRDT_OK) rc = fetch_merge_out(ctx, st, out, dout, dst->n_docs, dst->R, total);
     const int sync = crdt_ctx_sync(ctx, ctx->stream);
     return rc != CRDT_OK ? rc : sync;
 }

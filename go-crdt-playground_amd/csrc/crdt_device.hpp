@@ -20,6 +20,7 @@ constexpr uint32_t kErrWorkspace = 2u;  // fold scratch smaller than the output 
 constexpr uint32_t kErrHint = 4u;       // a doc broke the crdt_ctx_set_max_doc_entries promise
 constexpr uint32_t kErrCapacity = 8u;   // a doc's live count exceeds its slots (clamped)
 constexpr uint32_t kErrDupKey = 16u;    // a key appears twice in one document (ingest sort)
+constexpr uint32_t kErrUnsorted = 32u;  // keys not strictly ascending in a document (host path check)
 
 // Kernel-side view of an AWSet batch (same fields as crdt_awset_batch).
 struct BatchView {

@@ -371,6 +371,9 @@ inline Engine::Engine(int device) : batch_(new detail::Batch()) {
         delete batch_;
         throw Error(rc, "crdt_ctx_create");
     }
+    // results come back packed (live entries only): less to download, and the
+    // apply reads each document at out.offsets[d] either way
+    check(crdt_ctx_set_option(ctx_, "pack_batch_outputs", 1), "crdt_ctx_set_option");
 }
 inline Engine::~Engine() {
     crdt_ctx_destroy(ctx_);

@@ -158,7 +158,15 @@ int crdt_ctx_set_max_doc_entries(crdt_ctx* ctx, uint32_t max_entries);
  *   "join_nt_stores"      0|1         non-temporal output stores (default 1)
  *   "probe_blocks_per_cu" 1..64       crdt_bw_probe grid (default 16)
  *   (also "join_tile_capacity", "join_tile_shape", "join_tile_nt_stores",
- *   "join_tiles": see api.cpp) */
+ *   "join_tiles": see api.cpp)
+ * and one layout option of the host-buffer (*_batch) joins, exchanges and folds:
+ *   "pack_batch_outputs"  0|1         1: out holds only the live entries, doc d
+ *                                     at offsets[d] = counts[0] + .. + counts[d-1]
+ *                                     (less to download); 0 (default): at its
+ *                                     capacity offset, as the *_async calls write.
+ * The *_batch calls check the slot layout on the host and the key order on the
+ * device after the upload (CRDT_E_UNSORTED is then returned after the launch,
+ * the outputs unspecified); crdt_validate_batch checks everything on the host. */
 int crdt_ctx_set_option(crdt_ctx* ctx, const char* name, int64_t value);
 /* Wait for `stream`, return (and clear) the first device-side error. */
 int crdt_ctx_sync(crdt_ctx* ctx, void* stream);

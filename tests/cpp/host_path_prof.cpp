@@ -21,6 +21,7 @@ int crdt_ctx_create(int, crdt_ctx** out) {
     return CRDT_OK;
 }
 void crdt_ctx_destroy(crdt_ctx* c) { delete c; }
+int crdt_ctx_set_option(crdt_ctx*, const char*, int64_t) { return CRDT_OK; }
 const char* crdt_strerror(int) { return "error"; }
 int crdt_host_alloc(size_t bytes, void** out) {
     *out = malloc(bytes);

@@ -17,7 +17,7 @@ import pytest
 
 import crdtgpu
 from crdtgpu import CRDT_FOLD_AWSET, CRDT_FOLD_DELTA, workloads
-from crdtgpu.batch import OutBuffers, SrcBuffers
+from crdtgpu.batch import AWSetBatch, OutBuffers, SrcBatch, SrcBuffers
 from helpers import GOLDEN, batch_of, out_doc, outs_equal, random_state, snap_entries, src_batch_of
 from oracle import oracle
 
@@ -720,3 +720,77 @@ def test_graph_replay_stress_worklist_paths(torch, kind):
             assert_same_all(host_out(out, torch), want, n, R)
     finally:
         e.close()
+
+
+# ------------------------------------------------ host path: packed outputs, device order check
+
+@pytest.mark.parametrize("what", ["join", "exchange", "fold_awset", "fold_delta"])
+def test_packed_batch_outputs(torch, what):
+    """crdt_ctx_set_option("pack_batch_outputs", 1): the *_batch calls return
+    only live entries, doc d at the prefix sum of the counts; every document
+    bit-exact vs the oracle (large documents take the tile / block paths)."""
+    rng = random.Random(hash(what) % 1000)
+    R = 3
+    e = crdtgpu.Engine(0)
+    try:
+        e.set_option("pack_batch_outputs", 1)
+        if what in ("join", "exchange"):
+            dst, src = join_case(rng, 1500, R, lambda: rng.choice([0, 1, 30, 64, 65, 300, 3000]), 10 ** 6, 40)
+            if what == "join":
+                pairs = [(e.join(dst, src), oracle.join(dst, src))]
+            else:
+                g1, g2 = e.exchange(dst, src)
+                pairs = [(g1, oracle.join(dst, src)), (g2, oracle.join(src, dst))]
+        else:
+            mode = CRDT_FOLD_AWSET if what == "fold_awset" else CRDT_FOLD_DELTA
+            dst, srcs = fold_case(rng, 1500, R, lambda: rng.randint(0, 80), lambda: rng.randint(0, 6),
+                                  lambda: rng.randint(0, 12), lambda: rng.randint(0, 3), 300, 9, mode == CRDT_FOLD_DELTA)
+            pairs = [(e.fold(mode, dst, srcs), oracle.fold(mode, dst, srcs))]
+        for got, (rc, want) in pairs:
+            assert rc == 0
+            n = dst.n_docs
+            cnt = np.asarray(got.counts[:n]).astype(np.int64)
+            assert (np.asarray(got.offsets[: n + 1]) == np.concatenate([[0], np.cumsum(cnt)])).all()
+            for d in range(n):
+                assert out_doc(got, d, R) == out_doc(want, d, R), d
+    finally:
+        e.close()
+
+
+def test_batch_key_order_checked_on_device(eng):
+    """The *_batch calls check the key order after the upload (pack.hip): an
+    unsorted or repeated key in any document, source or tombstone list is
+    CRDT_E_UNSORTED, as crdt_validate_batch reports on the host."""
+    rng = random.Random(5)
+    R = 2
+    dst, src = join_case(rng, 300, R, lambda: rng.randint(2, 90), 10 ** 6, 9)
+    for which in ("dst", "src", "dup"):
+        d2, s2 = dst.numpy(), src.numpy()
+        b = d2 if which != "src" else s2
+        b = AWSetBatch(b.R, b.offsets.copy(), b.keys.copy(), b.actors, b.counters, b.vv, b.counts)
+        o = int(b.offsets[123])
+        if which == "dup":
+            b.keys[o + 1] = b.keys[o]
+        else:
+            b.keys[o], b.keys[o + 1] = b.keys[o + 1], b.keys[o]
+        assert crdtgpu.validate(b) == crdtgpu.CRDT_E_UNSORTED
+        with pytest.raises(crdtgpu.CrdtError) as ei:
+            if which == "src":
+                eng.join(d2, b)
+            else:
+                eng.exchange(b, s2)
+        assert ei.value.code == crdtgpu.CRDT_E_UNSORTED
+    fd, fs = fold_case(rng, 200, R, lambda: rng.randint(0, 20), lambda: rng.randint(1, 4), lambda: rng.randint(2, 9),
+                       lambda: rng.randint(2, 4), 300, 9, True)
+    for arr in ("keys", "tkeys"):
+        s = fs.numpy() if hasattr(fs, "numpy") else fs
+        bad = getattr(s, arr).copy()
+        k = int((s.entry_off if arr == "keys" else s.tomb_off)[5])
+        bad[k], bad[k + 1] = bad[k + 1], bad[k]
+        kw = {a: getattr(s, a) for a in ("doc_srcs", "src_actor", "vv", "entry_off", "keys", "actors", "counters",
+                                         "tomb_off", "tkeys", "tactors", "tcounters")}
+        kw[arr] = bad
+        s2 = SrcBatch(s.R, **kw)
+        with pytest.raises(crdtgpu.CrdtError) as ei:
+            eng.fold(CRDT_FOLD_DELTA, fd, s2)
+        assert ei.value.code == crdtgpu.CRDT_E_UNSORTED
