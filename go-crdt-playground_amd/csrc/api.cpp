@@ -3,7 +3,10 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdint>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <vector>
@@ -747,11 +750,20 @@ struct Stager {
     template <typename T>
     T* put(const T* host, size_t n) {  // allocate + copy in (n elements)
         if (rc != CRDT_OK) return nullptr;
+        static const bool trace = std::getenv("CRDT_TRACE_STAGE") != nullptr;  // diagnostics: host time per step
+        const auto t0 = std::chrono::steady_clock::now();
         DevBuf& b = ctx->stage[next++];
         rc = b.reserve(std::max<size_t>(n, 1) * sizeof(T));
         if (rc != CRDT_OK) return nullptr;
+        const auto t1 = std::chrono::steady_clock::now();
         if (host && n && hipMemcpyAsync(b.p, host, n * sizeof(T), hipMemcpyHostToDevice, ctx->stream) != hipSuccess)
             rc = CRDT_E_HIP;
+        if (trace) {
+            const auto t2 = std::chrono::steady_clock::now();
+            fprintf(stderr, "stage[%d] %zu B: reserve %.3f ms, copy call %.3f ms\n", next - 1, n * sizeof(T),
+                    std::chrono::duration<double, std::milli>(t1 - t0).count(),
+                    std::chrono::duration<double, std::milli>(t2 - t1).count());
+        }
         return b.as<T>();
     }
     template <typename T>
