@@ -252,7 +252,7 @@ class Config4(Config2):
 
     R = 2
     name = "config4"
-    kernel = "join_tile_kernel"
+    kernel = "join_tile_pipe_kernel"
     metric = "replica-merges/sec (AWSet join, Zipf sizes, config 4) + achieved HBM GB/s (% roofline)"
     cpu_docs = 96
 
@@ -285,8 +285,8 @@ class Config4(Config2):
 
     @property
     def kernel_name(self):
-        return ("join_tile_kernel (exchange call: join_wave_kernel for docs <= 64 per side, tile plan, merge-path "
-                "tiles of 2048 positions with look-back placement; timed as the whole call)")
+        return ("join_tile_pipe_kernel (exchange call: join_wave_kernel for docs <= 64 per side, tile plan, merge-path "
+                "tiles of 1024 positions placed by a look-back deferred by one tile; timed as the whole call)")
 
     def describe(self, world):
         return {"workload": "config4: %d docs/GPU, Zipf(1.1)-like sizes in [1, 2^20) (mean %.0f, max %d, %d entries "

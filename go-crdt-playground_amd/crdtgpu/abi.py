@@ -12,7 +12,8 @@ import os
 import re
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libcrdtgpu.so")
+# CRDTGPU_LIB: a diagnostic build of the same library (tools/libcrdtgpu_stamps.so)
+LIB_PATH = os.environ.get("CRDTGPU_LIB") or os.path.join(HERE, "libcrdtgpu.so")
 HEADER_PATH = os.path.join(os.path.dirname(os.path.dirname(HERE)), "include", "crdtgpu.h")
 
 CRDT_OK = 0

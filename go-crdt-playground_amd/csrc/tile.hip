@@ -160,7 +160,8 @@ __device__ __forceinline__ void flag_store(uint64_t* p, uint64_t v) {
 // Tile 0 of a document publishes its inclusive count at once, so the walk
 // ends inside the document; a predecessor not yet published is polled again
 // (it was dispensed before g and publishes its aggregate without waiting).
-__device__ __forceinline__ uint32_t look_back(uint64_t* flags, uint32_t g, uint32_t t, uint32_t lane) {
+__device__ __forceinline__ uint32_t look_back(uint64_t* flags, uint32_t g, uint32_t t, uint32_t lane,
+                                              uint64_t* polls = nullptr) {
     uint32_t prefix = 0;
     uint32_t look = g - 1;
     int32_t rem = (int32_t)t;
@@ -170,6 +171,7 @@ __device__ __forceinline__ uint32_t look_back(uint64_t* flags, uint32_t g, uint3
         const uint64_t inc = ballot(st == 2u);
         const uint32_t first_inc = inc ? (uint32_t)__builtin_ctzll(inc) : 64u;
         const uint64_t pending = ballot(st == 0u) & low_mask(first_inc + 1u);
+        if (polls) polls[pending ? 1 : 0] += 1;  // diagnostic builds: polls that found a gap / that summed
         if (pending) {
             __builtin_amdgcn_s_sleep(1);
             continue;
@@ -246,15 +248,20 @@ __device__ __forceinline__ TileGeo tile_geo(const BatchView& A, const TileWork& 
     return x;
 }
 
-// Issue a tile's loads into registers.  Thread tid holds staged positions
-// p = tid + q*NT: the dst run [0, nA), the src run [nA, n), and at p == n the
-// src element past the tile (a common key's twin across the boundary).  The
-// last thread also fetches that element when the tile is full (p == T) and
-// the dst key just before the tile.
+// One tile's operands in registers, loaded a tile ahead: thread tid holds staged
+// positions p = tid + q*NT -- the dst run [0, nA), the src run [nA, n), and at
+// p == n the src element past the tile (a common key's twin across the
+// boundary); the last thread also the element past a full tile (p == T) and the
+// dst key before the tile; lanes < R the two clocks.
+template <int IPT>
+struct TileRegs {
+    uint64_t k[IPT], c[IPT], xk, xc, pk, va, vb;
+    uint32_t a[IPT], xa;
+};
+
 template <int NT, int IPT>
 __device__ __forceinline__ void tile_issue(const BatchView& A, const BatchView& B, const TileGeo& x, uint32_t tid,
-                                           uint64_t (&rk)[IPT], uint32_t (&ra)[IPT], uint64_t (&rc)[IPT],
-                                           uint64_t& xk, uint32_t& xa, uint64_t& xc, uint64_t& pk) {
+                                           TileRegs<IPT>& r) {
     constexpr uint32_t T = NT * IPT;
     const uint32_t n = x.nA + x.nB;
     const bool peek = x.has_next;
@@ -270,29 +277,124 @@ __device__ __forceinline__ void tile_issue(const BatchView& A, const BatchView& 
         const bool inA = !x.bad && p < x.nA;
         const uint32_t pb = p - x.nA;
         const bool inB = !x.bad && !inA && (p < n || (p == n && peek));
-        rk[q] = inA ? __builtin_nontemporal_load(ak + p) : (inB ? __builtin_nontemporal_load(bk + pb) : 0ull);
-        ra[q] = inA ? __builtin_nontemporal_load(aa + p) : (inB ? __builtin_nontemporal_load(ba + pb) : 0u);
-        rc[q] = inA ? __builtin_nontemporal_load(ac + p) : (inB ? __builtin_nontemporal_load(bc + pb) : 0ull);
+        r.k[q] = inA ? __builtin_nontemporal_load(ak + p) : (inB ? __builtin_nontemporal_load(bk + pb) : 0ull);
+        r.a[q] = inA ? __builtin_nontemporal_load(aa + p) : (inB ? __builtin_nontemporal_load(ba + pb) : 0u);
+        r.c[q] = inA ? __builtin_nontemporal_load(ac + p) : (inB ? __builtin_nontemporal_load(bc + pb) : 0ull);
     }
-    xk = 0;
-    xa = 0;
-    xc = 0;
-    pk = 0;
+    r.xk = 0;
+    r.xa = 0;
+    r.xc = 0;
+    r.pk = 0;
     if (tid == NT - 1) {
         if (n == T && peek) {
-            xk = bk[x.nB];
-            xa = ba[x.nB];
-            xc = bc[x.nB];
+            r.xk = bk[x.nB];
+            r.xa = ba[x.nB];
+            r.xc = bc[x.nB];
         }
-        if (x.has_prev) pk = ak[-1];
+        if (x.has_prev) r.pk = ak[-1];
+    }
+    r.va = 0;
+    r.vb = 0;
+    if (!x.bad && tid < A.R) {
+        r.va = A.vv[(size_t)x.d * A.R + tid];
+        r.vb = B.vv[(size_t)x.d * A.R + tid];
     }
 }
 
-// Persistent workgroups take tiles in order from an atomic dispenser.  The
-// next tile is taken once this tile's look-back is done (from then on nothing
-// of this tile waits on another workgroup, so a taken tile is never held
-// behind a wait), and its loads are issued before this tile's output stores,
-// which they overlap.
+// Front of a tile: stage its registers in LDS, merge IPT positions per thread
+// from the thread's diagonal split deciding every union key, and compact the
+// survivors' LDS indices (out1 dot | out2 dot << 16) into sm.stage in merged
+// order.  Returns the tile's survivor count (every thread).  Ends with the
+// workgroup barrier of the scan.
+template <int NT, int IPT>
+__device__ __forceinline__ void tile_stage(TileSmem<NT, IPT>& sm, const TileGeo& cur, const TileRegs<IPT>& r,
+                                           uint32_t R, uint32_t tid) {
+    constexpr uint32_t T = NT * IPT;
+    const uint32_t nA = cur.nA, nB = cur.nB, n = nA + nB;  // n <= T
+#pragma unroll
+    for (int q = 0; q < IPT; ++q) {
+        const uint32_t p = tid + q * NT;
+        if (p <= n && p < T) {
+            sm.key[p] = r.k[q];
+            sm.act[p] = r.a[q];
+            sm.ctr[p] = r.c[q];
+        }
+    }
+    if (tid == NT - 1) {
+        if (n == T) {
+            sm.key[T] = r.xk;
+            sm.act[T] = r.xa;
+            sm.ctr[T] = r.xc;
+        }
+        sm.prev_key = r.pk;
+    }
+    if (tid < R) {
+        sm.va[tid] = r.va;
+        sm.vb[tid] = r.vb;
+    }
+}
+
+// The decide half of a tile's front (after tile_stage and a barrier).
+template <int NT, int IPT>
+__device__ __forceinline__ uint32_t tile_decide(TileSmem<NT, IPT>& sm, const TileGeo& cur, uint32_t R, uint32_t tid,
+                                                uint32_t& err) {
+    const uint32_t nA = cur.nA, nB = cur.nB, n = nA + nB;
+    const bool has_next = cur.has_next, has_prev = cur.has_prev;
+    const uint64_t prev_key = sm.prev_key;
+    const uint32_t k0 = min(tid * IPT, n);
+    uint32_t a = merge_path(sm.key, nA, sm.key + nA, nB, k0);
+    uint32_t b = k0 - a;
+    uint32_t pick[IPT];
+    bool keep[IPT];
+    uint32_t cnt = 0;
+#pragma unroll
+    for (int q = 0; q < IPT; ++q) {
+        keep[q] = false;
+        pick[q] = 0;
+        if (k0 + q < n) {
+            const bool take_a = a < nA && (b >= nB || sm.key[a] <= sm.key[nA + b]);
+            if (take_a) {
+                const uint64_t key = sm.key[a];
+                const uint32_t nb = b < nB ? nA + b : n;  // next src element (peeked past the tile)
+                const bool match = (b < nB || has_next) && sm.key[nb] == key;
+                if (match) {  // common key: present, src dot wins (awset.go:123-129,142)
+                    keep[q] = true;
+                    pick[q] = nb | (a << 16);
+                } else {  // dst-only: removed iff srcVV.HasDot(d) (awset.go:146-158)
+                    keep[q] = !has_dot(sm.vb, R, sm.act[a], sm.ctr[a], err);
+                    pick[q] = a | (a << 16);
+                }
+                ++a;
+            } else {
+                const uint32_t sb = nA + b;
+                const uint64_t key = sm.key[sb];
+                const bool match = a > 0 ? sm.key[a - 1] == key : (has_prev && prev_key == key);
+                if (!match) {  // src-only: added iff !dstVV.HasDot(s) (awset.go:130-140)
+                    keep[q] = !has_dot(sm.va, R, sm.act[sb], sm.ctr[sb], err);
+                    pick[q] = sb | (sb << 16);
+                }
+                ++b;
+            }
+            cnt += keep[q] ? 1u : 0u;
+        }
+    }
+    uint32_t agg;
+    const uint32_t lpos = block_exclusive_scan<NT>(cnt, sm.wave_tot, &agg);
+    uint32_t p = lpos;
+#pragma unroll
+    for (int q = 0; q < IPT; ++q)
+        if (keep[q]) sm.stage[p++] = pick[q];
+    return agg;
+}
+
+template <int NT, int IPT>
+__device__ __forceinline__ uint32_t tile_front(TileSmem<NT, IPT>& sm, const TileGeo& cur, const TileRegs<IPT>& r,
+                                               uint32_t R, uint32_t tid, uint32_t& err) {
+    tile_stage<NT, IPT>(sm, cur, r, R, tid);
+    __syncthreads();
+    return tile_decide<NT, IPT>(sm, cur, R, tid, err);
+}
+
 template <typename T, bool NTS>
 __device__ __forceinline__ void out_store(T v, T* p) {
     if (NTS)
@@ -301,17 +403,57 @@ __device__ __forceinline__ void out_store(T v, T* p) {
         *p = v;
 }
 
+// Survivors of a staged tile written coalesced at the document's output base +
+// prefix; the last tile writes the count, tile 0 the merged clock.
+template <int NT, int IPT, bool EXCH, bool NTS>
+__device__ __forceinline__ void tile_stores(const TileSmem<NT, IPT>& sm, const TileGeo& cur, uint32_t prefix,
+                                            uint32_t agg, uint32_t R, uint32_t tid, const OutView& o1,
+                                            const OutView& o2) {
+    if (cur.bad) return;
+    const size_t obase = (size_t)cur.obase + prefix;
+#pragma unroll
+    for (int q = 0; q < IPT; ++q) {
+        const uint32_t p = tid + q * NT;
+        if (p < agg) {
+            const uint32_t v = sm.stage[p];
+            const uint32_t x1 = v & 0xFFFFu, x2 = v >> 16;
+            const uint64_t key = sm.key[x1];
+            out_store<uint64_t, NTS>(key, o1.keys + obase + p);
+            out_store<uint32_t, NTS>(sm.act[x1], o1.actors + obase + p);
+            out_store<uint64_t, NTS>(sm.ctr[x1], o1.counters + obase + p);
+            if (EXCH) {
+                out_store<uint64_t, NTS>(key, o2.keys + obase + p);
+                out_store<uint32_t, NTS>(sm.act[x2], o2.actors + obase + p);
+                out_store<uint64_t, NTS>(sm.ctr[x2], o2.counters + obase + p);
+            }
+        }
+    }
+    if (cur.last && tid == 0) {
+        o1.counts[cur.d] = prefix + agg;
+        if (EXCH) o2.counts[cur.d] = prefix + agg;
+    }
+    if (cur.t == 0 && tid < R) {  // awset.go:160 -> crdt-misc.go:43-55, the same max both ways
+        const uint64_t m = max(sm.va[tid], sm.vb[tid]);
+        o1.vv[(size_t)cur.d * R + tid] = m;
+        if (EXCH) o2.vv[(size_t)cur.d * R + tid] = m;
+    }
+}
+
+// Persistent workgroups take tiles in order from an atomic dispenser.  The
+// next tile is taken once this tile's look-back is done (from then on nothing
+// of this tile waits on another workgroup, so a taken tile is never held
+// behind a wait), and its loads are issued before this tile's output stores,
+// which they overlap.
 template <int NT, int IPT, bool EXCH, bool NTS>
 __global__ __launch_bounds__(NT) void join_tile_kernel(BatchView A, BatchView B, OutView o1, OutView o2,
                                                        TileWork tw, Work wk) {
     __shared__ TileSmem<NT, IPT> sm;
-    constexpr uint32_t T = NT * IPT;
     const uint32_t tid = threadIdx.x, lane = tid & 63;
     const uint32_t R = A.R;
     const uint32_t total = *tw.total;
     uint32_t err = 0;
-    uint64_t rk[IPT], rc[IPT], xk, xc, pk;
-    uint32_t ra[IPT], xa;
+    TileRegs<IPT> rg;
+    STAMP_DECL
 
     if (tid == 0) sm.word[0] = atomicAdd(tw.head, 1u);
     __syncthreads();
@@ -319,84 +461,12 @@ __global__ __launch_bounds__(NT) void join_tile_kernel(BatchView A, BatchView B,
     TileGeo x{};
     if (g < total) {
         x = tile_geo(A, tw, g);
-        tile_issue<NT, IPT>(A, B, x, tid, rk, ra, rc, xk, xa, xc, pk);
+        tile_issue<NT, IPT>(A, B, x, tid, rg);
     }
     while (g < total) {
         const TileGeo cur = x;
-        const uint32_t nA = cur.nA, nB = cur.nB, n = nA + nB;  // n <= T
-        const uint32_t d = cur.d, t = cur.t;
-        // stage tile g: registers -> LDS
-#pragma unroll
-        for (int q = 0; q < IPT; ++q) {
-            const uint32_t p = tid + q * NT;
-            if (p <= n && p < T) {
-                sm.key[p] = rk[q];
-                sm.act[p] = ra[q];
-                sm.ctr[p] = rc[q];
-            }
-        }
-        if (tid == NT - 1) {
-            if (n == T) {
-                sm.key[T] = xk;
-                sm.act[T] = xa;
-                sm.ctr[T] = xc;
-            }
-            sm.prev_key = pk;
-        }
-        if (!cur.bad && tid < R) {
-            sm.va[tid] = A.vv[(size_t)d * R + tid];
-            sm.vb[tid] = B.vv[(size_t)d * R + tid];
-        }
-        __syncthreads();
-        const bool has_next = cur.has_next, has_prev = cur.has_prev;
-        const uint64_t prev_key = sm.prev_key;
-
-        // merge IPT positions from this thread's diagonal split
-        const uint32_t k0 = min(tid * IPT, n);
-        uint32_t a = merge_path(sm.key, nA, sm.key + nA, nB, k0);
-        uint32_t b = k0 - a;
-        uint32_t pick[IPT];
-        bool keep[IPT];
-        uint32_t cnt = 0;
-#pragma unroll
-        for (int q = 0; q < IPT; ++q) {
-            keep[q] = false;
-            pick[q] = 0;
-            if (k0 + q < n) {
-                const bool take_a = a < nA && (b >= nB || sm.key[a] <= sm.key[nA + b]);
-                if (take_a) {
-                    const uint64_t key = sm.key[a];
-                    const uint32_t nb = b < nB ? nA + b : n;  // next src element (peeked past the tile)
-                    const bool match = (b < nB || has_next) && sm.key[nb] == key;
-                    if (match) {  // common key: present, src dot wins (awset.go:123-129,142)
-                        keep[q] = true;
-                        pick[q] = nb | (a << 16);
-                    } else {  // dst-only: removed iff srcVV.HasDot(d) (awset.go:146-158)
-                        keep[q] = !has_dot(sm.vb, R, sm.act[a], sm.ctr[a], err);
-                        pick[q] = a | (a << 16);
-                    }
-                    ++a;
-                } else {
-                    const uint32_t sb = nA + b;
-                    const uint64_t key = sm.key[sb];
-                    const bool match = a > 0 ? sm.key[a - 1] == key : (has_prev && prev_key == key);
-                    if (!match) {  // src-only: added iff !dstVV.HasDot(s) (awset.go:130-140)
-                        keep[q] = !has_dot(sm.va, R, sm.act[sb], sm.ctr[sb], err);
-                        pick[q] = sb | (sb << 16);
-                    }
-                    ++b;
-                }
-                cnt += keep[q] ? 1u : 0u;
-            }
-        }
-        uint32_t agg;
-        const uint32_t lpos = block_exclusive_scan<NT>(cnt, sm.wave_tot, &agg);
-        {
-            uint32_t p = lpos;
-#pragma unroll
-            for (int q = 0; q < IPT; ++q)
-                if (keep[q]) sm.stage[p++] = pick[q];
-        }
+        const uint32_t agg = tile_front<NT, IPT>(sm, cur, rg, R, tid, err);
+        STAMP(1)
         if (tid < 64) {
             uint32_t prefix = 0;
             if (cur.bad) {
@@ -404,13 +474,11 @@ __global__ __launch_bounds__(NT) void join_tile_kernel(BatchView A, BatchView B,
                     atomicOr(wk.status, kErrWorkspace);
                     flag_store(tw.flags + g, kFlagInc);
                 }
-            } else if (t == 0) {
+            } else if (cur.t == 0) {
                 if (lane == 0) flag_store(tw.flags + g, kFlagInc | agg);
             } else {
                 if (lane == 0) flag_store(tw.flags + g, kFlagAgg | agg);
-            }
-            if (!cur.bad && t != 0) {
-                prefix = look_back(tw.flags, g, t, lane);
+                prefix = look_back(tw.flags, g, cur.t, lane);
                 if (lane == 0) flag_store(tw.flags + g, kFlagInc | (prefix + agg));
             }
             // nothing of this tile waits on another workgroup any more: take the
@@ -422,44 +490,109 @@ __global__ __launch_bounds__(NT) void join_tile_kernel(BatchView A, BatchView B,
             }
         }
         __syncthreads();
+        STAMP(3)
         const uint32_t prefix = sm.word[1];
         const uint32_t gn = sm.word[0];
         if (gn < total) {  // the next tile's loads overlap this tile's stores
             x = tile_geo(A, tw, gn);
-            tile_issue<NT, IPT>(A, B, x, tid, rk, ra, rc, xk, xa, xc, pk);
+            tile_issue<NT, IPT>(A, B, x, tid, rg);
         }
-        if (!cur.bad) {
-            const size_t obase = (size_t)cur.obase + prefix;
-#pragma unroll
-            for (int q = 0; q < IPT; ++q) {
-                const uint32_t p = tid + q * NT;
-                if (p < agg) {
-                    const uint32_t v = sm.stage[p];
-                    const uint32_t x1 = v & 0xFFFFu, x2 = v >> 16;
-                    const uint64_t key = sm.key[x1];
-                    out_store<uint64_t, NTS>(key, o1.keys + obase + p);
-                    out_store<uint32_t, NTS>(sm.act[x1], o1.actors + obase + p);
-                    out_store<uint64_t, NTS>(sm.ctr[x1], o1.counters + obase + p);
-                    if (EXCH) {
-                        out_store<uint64_t, NTS>(key, o2.keys + obase + p);
-                        out_store<uint32_t, NTS>(sm.act[x2], o2.actors + obase + p);
-                        out_store<uint64_t, NTS>(sm.ctr[x2], o2.counters + obase + p);
-                    }
-                }
+        STAMP(4)
+        tile_stores<NT, IPT, EXCH, NTS>(sm, cur, prefix, agg, R, tid, o1, o2);
+        __syncthreads();
+        STAMP(5)
+        g = gn;
+    }
+    STAMP_FLUSH
+    if (__syncthreads_or(err != 0) && tid == 0) atomicOr(wk.status, kErrActorRange);
+}
+
+// Pipelined tiles: a tile's look-back is deferred by one tile.  Per round the
+// workgroup (1) decides tile g1 (its loads arrived during the previous round)
+// and publishes g1's aggregate at once, (2) runs the look-back of the tile
+// before it, g0, whose predecessors have had a whole front to publish, (3) takes
+// the next tile g2 and issues its loads, (4) writes g0's survivors.  Two LDS
+// tile buffers alternate.  Holding: g1 is held through g0's look-back with its
+// aggregate already published (successors sum past it); g2 is taken after the
+// look-back and decided next round with nothing to wait on in between -- so
+// every walk ends (each tile's aggregate is published without waiting, and
+// tile 0 of a document publishes its inclusive count).
+template <int NT, int IPT, bool EXCH, bool NTS>
+__global__ __launch_bounds__(NT) void join_tile_pipe_kernel(BatchView A, BatchView B, OutView o1, OutView o2,
+                                                            TileWork tw, Work wk) {
+    __shared__ TileSmem<NT, IPT> sm[2];
+    __shared__ uint32_t word[2];
+    const uint32_t tid = threadIdx.x, lane = tid & 63;
+    const uint32_t R = A.R;
+    const uint32_t total = *tw.total;
+    uint32_t err = 0;
+    TileRegs<IPT> rg;
+    STAMP_DECL
+
+    if (tid == 0) word[0] = atomicAdd(tw.head, 1u);
+    __syncthreads();
+    uint32_t g1 = word[0];
+    if (g1 >= total) return;
+    TileGeo x1 = tile_geo(A, tw, g1);
+    tile_issue<NT, IPT>(A, B, x1, tid, rg);
+    uint32_t g0 = total, agg0 = 0;  // g0 >= total: no tile waiting for its stores
+    TileGeo x0{};
+    uint32_t buf = 0;
+    // g0's look-back (wave 0), then the next tile; every thread gets both
+    auto resolve0 = [&](uint32_t& prefix0, uint32_t& g2) {
+        if (tid < 64) {
+            uint32_t p0 = 0;
+            if (g0 < total && !x0.bad && x0.t != 0) {
+                p0 = look_back(tw.flags, g0, x0.t, lane);
+                if (lane == 0) flag_store(tw.flags + g0, kFlagInc | (p0 + agg0));
             }
-            if (cur.last && tid == 0) {
-                o1.counts[d] = prefix + agg;
-                if (EXCH) o2.counts[d] = prefix + agg;
-            }
-            if (t == 0 && tid < R) {  // awset.go:160 -> crdt-misc.go:43-55, the same max both ways
-                const uint64_t m = max(sm.va[tid], sm.vb[tid]);
-                o1.vv[(size_t)d * R + tid] = m;
-                if (EXCH) o2.vv[(size_t)d * R + tid] = m;
+            if (lane == 0) {
+                word[1] = p0;
+                word[0] = atomicAdd(tw.head, 1u);
             }
         }
         __syncthreads();
-        g = gn;
+        prefix0 = word[1];
+        g2 = word[0];
+    };
+    auto publish1 = [&](uint32_t agg1) {
+        if (tid == 0) {  // publish g1 at once: inclusive for a document's first tile
+            if (x1.bad) {
+                atomicOr(wk.status, kErrWorkspace);
+                flag_store(tw.flags + g1, kFlagInc);
+            } else {
+                flag_store(tw.flags + g1, (x1.t == 0 ? kFlagInc : kFlagAgg) | agg1);
+            }
+        }
+    };
+    for (;;) {
+        const bool have1 = g1 < total, have0 = g0 < total;
+        uint32_t agg1 = 0, prefix0 = 0, g2 = total;
+        if (have1) {
+            agg1 = tile_front<NT, IPT>(sm[buf], x1, rg, R, tid, err);
+            publish1(agg1);
+        }
+        STAMP(1)
+        resolve0(prefix0, g2);
+        STAMP(3)
+        TileGeo x2{};
+        if (g2 < total) {  // g2's loads overlap g0's stores
+            x2 = tile_geo(A, tw, g2);
+            tile_issue<NT, IPT>(A, B, x2, tid, rg);
+        }
+        STAMP(4)
+        if (have0) tile_stores<NT, IPT, EXCH, NTS>(sm[buf ^ 1], x0, prefix0, agg0, R, tid, o1, o2);
+        if (!have1 && g2 >= total) break;  // (g2 >= total whenever g1 is: the dispenser only grows)
+        __syncthreads();
+        STAMP(5)
+        g0 = g1;
+        x0 = x1;
+        agg0 = agg1;
+        g1 = g2;
+        x1 = x2;
+        buf ^= 1u;
     }
+    STAMP_FLUSH
     if (__syncthreads_or(err != 0) && tid == 0) atomicOr(wk.status, kErrActorRange);
 }
 
@@ -478,10 +611,41 @@ static hipError_t launch_tile_kernel_s(const BatchView& A, const BatchView& B, c
     }
     const dim3 grid(n_cu * per_cu);
     if (o2)
-        hipLaunchKernelGGL((join_tile_kernel<NT, IPT, true, NTS>), grid, dim3(NT), 0, stream, A, B, o1, *o2, tw, wk);
+        hipLaunchKernelGGL((join_tile_kernel<NT, IPT, true, NTS>), grid, dim3(NT), 0, stream, A, B, o1, *o2, tw,
+                           wk);
     else
-        hipLaunchKernelGGL((join_tile_kernel<NT, IPT, false, NTS>), grid, dim3(NT), 0, stream, A, B, o1, o1, tw, wk);
+        hipLaunchKernelGGL((join_tile_kernel<NT, IPT, false, NTS>), grid, dim3(NT), 0, stream, A, B, o1, o1, tw,
+                           wk);
     return hipGetLastError();
+}
+
+template <int NT, int IPT, bool NTS>
+static hipError_t launch_tile_pipe_s(const BatchView& A, const BatchView& B, const OutView& o1, const OutView* o2,
+                                     const Work& wk, const TileWork& tw, uint32_t n_cu, hipStream_t stream) {
+    static int per_cu = 0;  // resident workgroups per CU (occupancy query, once per shape)
+    if (per_cu == 0) {
+        int nb = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, join_tile_pipe_kernel<NT, IPT, true, NTS>, NT, 0) !=
+                hipSuccess ||
+            nb < 1)
+            nb = 1;
+        per_cu = nb;
+    }
+    const dim3 grid(n_cu * per_cu);
+    if (o2)
+        hipLaunchKernelGGL((join_tile_pipe_kernel<NT, IPT, true, NTS>), grid, dim3(NT), 0, stream, A, B, o1, *o2, tw,
+                           wk);
+    else
+        hipLaunchKernelGGL((join_tile_pipe_kernel<NT, IPT, false, NTS>), grid, dim3(NT), 0, stream, A, B, o1, o1, tw,
+                           wk);
+    return hipGetLastError();
+}
+
+template <int NT, int IPT>
+static hipError_t launch_tile_pipe(const BatchView& A, const BatchView& B, const OutView& o1, const OutView* o2,
+                                   const Work& wk, const TileWork& tw, uint32_t n_cu, hipStream_t stream) {
+    return tw.nt_stores ? launch_tile_pipe_s<NT, IPT, true>(A, B, o1, o2, wk, tw, n_cu, stream)
+                        : launch_tile_pipe_s<NT, IPT, false>(A, B, o1, o2, wk, tw, n_cu, stream);
 }
 
 template <int NT, int IPT>
@@ -496,6 +660,10 @@ uint32_t tile_positions(uint32_t shape) {
         case 1: return 256 * 4;
         case 2: return 256 * 8;
         case 3: return 1024 * 2;
+        case 4: return 256 * 4;  // pipelined look-back (join_tile_pipe_kernel)
+        case 5: return 512 * 2;
+        case 6: return 256 * 8;
+        case 7: return 128 * 8;
         default: return 512 * 4;
     }
 }
@@ -521,8 +689,25 @@ hipError_t launch_join_tiles(const BatchView& A, const BatchView& B, const OutVi
         case 1: return launch_tile_kernel<256, 4>(A, B, o1, o2, wk, tw, n_cu, stream);
         case 2: return launch_tile_kernel<256, 8>(A, B, o1, o2, wk, tw, n_cu, stream);
         case 3: return launch_tile_kernel<1024, 2>(A, B, o1, o2, wk, tw, n_cu, stream);
+        case 4: return launch_tile_pipe<256, 4>(A, B, o1, o2, wk, tw, n_cu, stream);
+        case 5: return launch_tile_pipe<512, 2>(A, B, o1, o2, wk, tw, n_cu, stream);
+        case 6: return launch_tile_pipe<256, 8>(A, B, o1, o2, wk, tw, n_cu, stream);
+        case 7: return launch_tile_pipe<128, 8>(A, B, o1, o2, wk, tw, n_cu, stream);
         default: return launch_tile_kernel<512, 4>(A, B, o1, o2, wk, tw, n_cu, stream);
     }
 }
 
 }  // namespace crdt
+
+#ifdef CRDT_STAMPS
+// Diagnostic builds only (Makefile target "stamps"): the tile kernel's phase
+// cycles summed over waves, read and optionally cleared.
+extern "C" int crdt_probe_tile_stamps(unsigned long long* out, int reset) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(crdt::g_stamps), 16 * sizeof(unsigned long long)) != hipSuccess) return -1;
+    if (reset) {
+        static const unsigned long long z[16] = {0};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(crdt::g_stamps), z, sizeof(z)) != hipSuccess) return -1;
+    }
+    return 0;
+}
+#endif

@@ -42,6 +42,21 @@ def eng(torch):
     e.close()
 
 
+# every tile shape (threads x positions; look-back per tile or deferred by one)
+# must give the same bits
+SHAPES = [4, 0, 1, 2, 3, 5, 6, 7]
+
+
+@pytest.fixture(params=SHAPES, ids=lambda s: "shape%d" % s)
+def shaped(eng, request):
+    eng.set_option("join_tile_shape", request.param)
+    yield eng
+    eng.set_option("join_tile_shape", DEFAULT_SHAPE)
+
+
+DEFAULT_SHAPE = 4
+
+
 def interleaved(rng, n, R, share):
     """Two states over one key range: a fraction `share` of dst's keys also in
     src, so common pairs fall on every tile boundary sooner or later."""
@@ -69,7 +84,7 @@ def check_join_and_exchange(eng, dst, src, R):
 
 
 @pytest.mark.parametrize("n", [TILE // 2 - 1, TILE // 2, TILE // 2 + 1, TILE - 1, TILE, TILE + 1, 3 * TILE + 7])
-def test_tile_boundaries_split_common_pairs(eng, n):
+def test_tile_boundaries_split_common_pairs(shaped, n):
     """Sizes around multiples of the tile; common keys everywhere; both HasDot
     sides live (dots above and below the other side's clock)."""
     rng = random.Random(n)
@@ -80,10 +95,10 @@ def test_tile_boundaries_split_common_pairs(eng, n):
         docs_d.append(d)
         docs_s.append(s)
     dst, src = batch_of(R, docs_d), batch_of(R, docs_s)
-    check_join_and_exchange(eng, dst, src, R)
+    check_join_and_exchange(shaped, dst, src, R)
 
 
-def test_tile_equal_key_sets(eng):
+def test_tile_equal_key_sets(shaped):
     """Identical key sets: every dst element is followed by its src twin, so the
     merge path cuts between twins at every odd tile boundary."""
     rng = random.Random(5)
@@ -93,10 +108,10 @@ def test_tile_equal_key_sets(eng):
         keys = sorted(rng.sample(range(10 ** 9), n))
         docs_d.append(([(k, rng.randrange(2), rng.randint(1, 9)) for k in keys], [5, 5]))
         docs_s.append(([(k, rng.randrange(2), rng.randint(1, 9)) for k in keys], [4, 6]))
-    check_join_and_exchange(eng, batch_of(R, docs_d), batch_of(R, docs_s), R)
+    check_join_and_exchange(shaped, batch_of(R, docs_d), batch_of(R, docs_s), R)
 
 
-def test_tile_mixed_with_small_docs_and_slack(eng, torch):
+def test_tile_mixed_with_small_docs_and_slack(shaped, torch):
     """Small (wave path) and large (tile path) documents in one batch, counts <
     slots on both inputs, device-resident through the async ABI."""
     rng = random.Random(7)
@@ -109,12 +124,12 @@ def test_tile_mixed_with_small_docs_and_slack(eng, torch):
     assert rc == 0
     dev = torch.device("cuda:0")
     out = OutBuffers(dst.n_docs, R, int(dst.offsets[-1]) + int(src.offsets[-1]), device=dev)
-    eng.join_async(dst.to(dev), src.to(dev), out)
-    eng.sync()
+    shaped.join_async(dst.to(dev), src.to(dev), out)
+    shaped.sync()
     assert_same(host_out(out, torch), want, dst.n_docs, R)
 
 
-def test_tile_one_document_of_a_million(eng):
+def test_tile_one_document_of_a_million(shaped):
     """One 2^20 + 2^20 document (1,024 tiles in one look-back chain)."""
     rng = np.random.default_rng(9)
     R = 2
@@ -129,7 +144,7 @@ def test_tile_one_document_of_a_million(eng):
                           rng.integers(0, 1000, R).astype(np.uint64))
 
     a, b = side(pick()), side(pick())
-    check_join_and_exchange(eng, a, b, R)
+    check_join_and_exchange(shaped, a, b, R)
 
 
 def test_tile_fallback_and_switch(eng):

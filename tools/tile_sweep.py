@@ -30,12 +30,15 @@ def main():
     o1, o2 = OutBuffers(n, 2, 2 * total, device=dev), OutBuffers(n, 2, 2 * total, device=dev)
     a, b = A.as_batch(), B.as_batch()
     ref = None
-    for shape, nts in ((2, 0), (2, 1), (0, 0), (0, 1), (1, 0), (3, 0), (2, 0)):
+    shapes = [tuple(int(v) for v in a.split(":")) for a in sys.argv[2:]] or \
+        [(2, 1), (4, 1), (8, 1), (5, 1), (9, 1), (8, 0), (4, 1), (8, 1), (2, 1)]
+    for shape, nts in shapes:
         eng.set_option("join_tile_shape", shape)
         eng.set_option("join_tile_nt_stores", nts)
         eng.exchange_async(a, b, o1, o2)
         eng.sync()
-        got = (o1.counts.clone(), o1.keys[:: 9973].clone(), o2.counters[:: 9973].clone())
+        got = (o1.counts.clone(), o1.keys.clone(), o1.actors.clone(), o1.counters.clone(), o2.counts.clone(),
+               o2.keys.clone(), o2.actors.clone(), o2.counters.clone(), o1.vv.clone(), o2.vv.clone())
         if ref is None:
             ref = got
         same = all(torch.equal(x, y) for x, y in zip(ref, got))
