@@ -318,7 +318,8 @@ class Config3:
     M = 10
     name = "config3"
     kernel = "fold_pipe_kernel"
-    kernel_name = "fold_pipe_kernel<32, true> (per-document fold, delta)"
+    kernel_name = ("fold_pipe_kernel<32, true, true, false> (per-document fold, delta: lean slot-walk pass, then the "
+                   "general pass over the documents it defers; timed as the whole call)")
     metric = "replica-merges/sec (AWSetDelta fold, config 3) + achieved HBM GB/s (% roofline)"
     mode = 1  # CRDT_FOLD_DELTA
     cpu_docs = 32768
@@ -393,7 +394,7 @@ class Config5(Config3):
     E = 16
     name = "config5"
     kernel = "fold_pipe_kernel"
-    kernel_name = "fold_pipe_kernel<32, false> (per-document fold, awset)"
+    kernel_name = "fold_pipe_kernel<32, false, false, false> (per-document fold, awset)"
     metric = "replica-merges/sec (AWSet fold r0<-..<-r7, config 5) + achieved HBM GB/s (% roofline)"
     mode = 0  # CRDT_FOLD_AWSET
     cpu_docs = 32768

@@ -19,7 +19,7 @@ hipError_t launch_join(const BatchView& dst, const BatchView& src, const OutView
                        const Work& wk, uint32_t docs_per_wave, bool nt_stores, uint32_t block_grid, bool no_large,
                        const TileWork* tw, uint32_t n_cu, hipStream_t stream);
 hipError_t launch_fold(int mode, const BatchView& dst, const SrcView& sb, const OutView& out, const Scratch& scr,
-                       const Work& wk, uint32_t block_grid, hipStream_t stream);
+                       const Work& wk, uint32_t block_grid, bool lean_first, hipStream_t stream);
 uint32_t tile_positions(uint32_t shape);
 hipError_t sort_storage(uint32_t n_docs, uint32_t n_slots, size_t* bytes);
 hipError_t launch_check_order(const uint32_t* off, const uint32_t* cnt, uint32_t n, const uint64_t* keys,
@@ -110,6 +110,7 @@ struct crdt_ctx {
     // zeroed by every call; [64,68): status word, cleared by crdt_ctx_sync.
     DevBuf ws;
     DevBuf worklist;
+    DevBuf defer;  // folds: documents the lean pass leaves to the general kernel
     DevBuf parts;
     DevBuf scratch;  // fold block path ping-pong: keys | actors | counters
     // large-document join tiles (tile.hip): descriptors + look-back words for
@@ -124,6 +125,7 @@ struct crdt_ctx {
     uint32_t max_doc_entries = 0xFFFFFFFFu;  // caller's promise (crdt_ctx_set_max_doc_entries)
     uint32_t join_docs_per_wave = 8;          // crdt_ctx_set_option("join_docs_per_wave")
     bool join_nt_stores = true;               // crdt_ctx_set_option("join_nt_stores")
+    bool fold_lean_first = true;              // crdt_ctx_set_option("fold_lean_first")
     uint32_t probe_blocks_per_cu = 16;        // crdt_ctx_set_option("probe_blocks_per_cu")
     bool pack_outputs = false;                // crdt_ctx_set_option("pack_batch_outputs")
     // staging for the *_batch host path
@@ -167,6 +169,8 @@ Work make_work(crdt_ctx* ctx) {
     w.status = ctx->ws.as<uint32_t>(64);
     w.chunk_ctr = ctx->ws.as<uint32_t>(32);
     w.worklist = ctx->worklist.as<uint32_t>();
+    w.defer_count = ctx->ws.as<uint32_t>(8);
+    w.defer = ctx->defer.as<uint32_t>();
     return w;
 }
 
@@ -203,7 +207,9 @@ int grow(DevBuf& b, size_t want, bool capturing) {
 }
 
 int reserve_worklist(crdt_ctx* ctx, uint32_t n_docs) {
-    return ctx->worklist.reserve(std::max<size_t>((size_t)n_docs, 1) * sizeof(uint32_t));
+    int rc = ctx->worklist.reserve(std::max<size_t>((size_t)n_docs, 1) * sizeof(uint32_t));
+    if (rc == CRDT_OK) rc = ctx->defer.reserve(std::max<size_t>((size_t)n_docs, 1) * sizeof(uint32_t));
+    return rc;
 }
 
 int reserve_scratch(crdt_ctx* ctx, uint64_t slots) {
@@ -267,7 +273,7 @@ int crdt_ctx_create(int device, crdt_ctx** out) {
     crdt_ctx* ctx = new (std::nothrow) crdt_ctx();
     if (!ctx) return CRDT_E_NOMEM;
     ctx->device = device;
-    for (DevBuf* b : {&ctx->ws, &ctx->worklist, &ctx->parts, &ctx->scratch, &ctx->tile_desc, &ctx->tile_geo, &ctx->tile_flags,
+    for (DevBuf* b : {&ctx->ws, &ctx->worklist, &ctx->defer, &ctx->parts, &ctx->scratch, &ctx->tile_desc, &ctx->tile_geo, &ctx->tile_flags,
                       &ctx->tile_slot, &ctx->tile_run, &ctx->sort_tmp, &ctx->sort_idx, &ctx->sort_ends})
         b->retired = &ctx->retired;
     for (auto& b : ctx->stage) b.retired = &ctx->retired;
@@ -302,6 +308,7 @@ void crdt_ctx_destroy(crdt_ctx* ctx) {
     ctx->retired.clear();
     ctx->ws.release();
     ctx->worklist.release();
+    ctx->defer.release();
     ctx->parts.release();
     ctx->scratch.release();
     for (DevBuf* b : {&ctx->tile_desc, &ctx->tile_geo, &ctx->tile_flags, &ctx->tile_slot, &ctx->tile_run,
@@ -358,6 +365,10 @@ int crdt_ctx_set_option(crdt_ctx* ctx, const char* name, int64_t value) {
     if (!strcmp(name, "probe_blocks_per_cu")) {
         if (value < 1 || value > 64) return CRDT_E_INVALID;
         ctx->probe_blocks_per_cu = (uint32_t)value;
+        return CRDT_OK;
+    }
+    if (!strcmp(name, "fold_lean_first")) {  // delta folds: slot-walk pass first, the rest deferred (fold.hip)
+        ctx->fold_lean_first = value != 0;
         return CRDT_OK;
     }
     if (!strcmp(name, "join_nt_stores")) {
@@ -450,6 +461,7 @@ int crdt_awset_fold_async(crdt_ctx* ctx, int mode, const crdt_awset_batch* dst, 
     bool cap = false;
     rc = enter(ctx, s, cap);
     if (rc == CRDT_OK) rc = grow(ctx->worklist, std::max<size_t>(dst->n_docs, 1) * sizeof(uint32_t), cap);
+    if (rc == CRDT_OK) rc = grow(ctx->defer, std::max<size_t>(dst->n_docs, 1) * sizeof(uint32_t), cap);
     if (rc != CRDT_OK) return rc;
     if (ctx->scratch_slots == 0) {
         if (cap) return CRDT_E_WORKSPACE;
@@ -459,7 +471,8 @@ int crdt_awset_fold_async(crdt_ctx* ctx, int mode, const crdt_awset_batch* dst, 
     const size_t slots = ctx->scratch_slots;
     Scratch scr{ctx->scratch.as<uint64_t>(0), ctx->scratch.as<uint32_t>(slots * 16), ctx->scratch.as<uint64_t>(slots * 8),
                 slots};
-    rc = hip_err(launch_fold(mode, view(dst), view(srcs), view(out), scr, make_work(ctx), block_grid(ctx), s));
+    rc = hip_err(launch_fold(mode, view(dst), view(srcs), view(out), scr, make_work(ctx), block_grid(ctx),
+                             ctx->fold_lean_first, s));
     return leave(ctx, s, cap, rc);
 }
 

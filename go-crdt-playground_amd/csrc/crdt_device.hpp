@@ -72,6 +72,8 @@ struct Work {
     uint32_t* wl_head;     // dequeue head of the block path
     uint32_t* worklist;    // [n_docs]
     uint32_t* chunk_ctr;   // [8] chunk dispenser shards of the wave path
+    uint32_t* defer;       // [n_docs] folds: documents the lean pass leaves to the general one
+    uint32_t* defer_count; // number of deferred documents
 };
 
 // Batched local ops (apply.hip): the op lists, tombstones in and out.
@@ -257,6 +259,15 @@ __device__ __forceinline__ void push_work(const Work& wk, uint32_t d, uint32_t n
     const uint32_t slot = atomicAdd(wk.wl_count, 1u);
     if (slot < n_docs)
         wk.worklist[slot] = d;
+    else
+        atomicOr(wk.status, kErrWorkspace);
+}
+
+// Defer a document from the lean fold pass to the general one (same bounds as push_work).
+__device__ __forceinline__ void push_defer(const Work& wk, uint32_t d, uint32_t n_docs) {
+    const uint32_t slot = atomicAdd(wk.defer_count, 1u);
+    if (slot < n_docs)
+        wk.defer[slot] = d;
     else
         atomicOr(wk.status, kErrWorkspace);
 }

@@ -64,12 +64,22 @@ namespace crdt {
 // tuples -- fewer registers for the prefetch and the walk, so the kernel fits
 // 128 VGPRs with no spills; larger documents take the block kernel).  VCH:
 // 64-word chunks of source clocks.
-template <bool DELTA>
+//
+// LEAN (delta folds): the pass that resolves a document only by the slot walk
+// (dense_delta_walk) -- no sort paths, so 128 VGPRs and 192 clock words: 4 waves
+// per SIMD.  A document it cannot walk (key span >= 256, > 15 sources, an
+// actor == len(VV), or beyond its tuple / clock capacity) is deferred, untouched,
+// to the general kernel, which takes the deferred list (LIST) afterwards.
+#ifndef CRDT_FOLD_LEAN_WPE
+#define CRDT_FOLD_LEAN_WPE 4
+#endif
+template <bool DELTA, bool LEAN = false>
 struct FoldShape {
-    static constexpr int WPE = DELTA ? CRDT_FOLD_DELTA_WPE : CRDT_FOLD_AWSET_WPE;
+    static constexpr int WPE = LEAN ? CRDT_FOLD_LEAN_WPE : (DELTA ? CRDT_FOLD_DELTA_WPE : CRDT_FOLD_AWSET_WPE);
     static constexpr int NCH = DELTA ? 4 : 2;
-    static constexpr int VCH = DELTA ? 4 : 2;
-    static constexpr int VCAP = (DELTA && CRDT_FOLD_DELTA_WPE < 4) ? 256 : (DELTA ? 224 : 128);
+    static constexpr int VCH = LEAN ? 3 : (DELTA ? 4 : 2);
+    static constexpr int VCAP =
+        LEAN ? 192 : ((DELTA && CRDT_FOLD_DELTA_WPE < 4) ? 256 : (DELTA ? 224 : 128));
 };
 
 template <int VCAP_, int NCAP_>
@@ -657,10 +667,11 @@ constexpr int kFoldK = 32;     // consecutive documents per wavefront
 // stores of one document's write-out: walk rounds x 3 + count + VV
 __host__ __device__ constexpr int fold_stores(int nch) { return nch * 3 + 2; }
 
-template <int K, bool DELTA>
-__global__ __launch_bounds__(kFoldWaves * 64) __attribute__((amdgpu_waves_per_eu(FoldShape<DELTA>::WPE))) void fold_pipe_kernel(BatchView dst, SrcView sb, OutView out, Work wk) {
-    constexpr int NCH = FoldShape<DELTA>::NCH, VCH = FoldShape<DELTA>::VCH;
-    using Smem = FoldSmem<FoldShape<DELTA>::VCAP, 64 * NCH>;
+template <int K, bool DELTA, bool LEAN, bool LIST>
+__global__ __launch_bounds__(kFoldWaves * 64) __attribute__((amdgpu_waves_per_eu(FoldShape<DELTA, LEAN>::WPE))) void fold_pipe_kernel(BatchView dst, SrcView sb, OutView out, Work wk) {
+    static_assert(!(LEAN && LIST), "the lean pass runs over consecutive documents");
+    constexpr int NCH = FoldShape<DELTA, LEAN>::NCH, VCH = FoldShape<DELTA, LEAN>::VCH;
+    using Smem = FoldSmem<FoldShape<DELTA, LEAN>::VCAP, 64 * NCH>;
     __shared__ Smem smem[kFoldWaves];
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t w = threadIdx.x >> 6;
@@ -672,31 +683,54 @@ __global__ __launch_bounds__(kFoldWaves * 64) __attribute__((amdgpu_waves_per_eu
     uint32_t err = 0;
     STAMP_DECL
 
+    // LIST: the run is entries [first, first + K) of the deferred list
+    const uint32_t n_run = LIST ? min(__hip_atomic_load(wk.defer_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                                      n_docs)
+                                : n_docs;
     const uint32_t first = uniform((blockIdx.x * kFoldWaves + w) * (uint32_t)K);
-    if (first >= n_docs) return;
-    const uint32_t cnt = min((uint32_t)K, n_docs - first);
+    if (first >= n_run) return;
+    const uint32_t cnt = min((uint32_t)K, n_run - first);
 
-    // ---- metadata of the run: lane i <= cnt describes document first + i
-    const uint32_t di = first + min(lane, cnt);
+    // ---- metadata of the run: lane i <= cnt describes document first + i (LIST:
+    // lane i < cnt describes deferred document i, with its end bounds loaded)
+    const uint32_t di = LIST ? wk.defer[first + min(lane, cnt - 1u)] : first + min(lane, cnt);
     const uint32_t mv_ds = sb.doc_srcs[di];
     const uint32_t mv_off = dst.offsets[di];
     const uint32_t mv_cnt = dst.counts ? dst.counts[min(di, n_docs - 1u)] : 0u;
     const uint32_t mv_eo = sb.entry_off[mv_ds];
     const uint32_t mv_to = tombs ? sb.tomb_off[mv_ds] : 0u;
-    const uint32_t slots_i = (uint32_t)__shfl_down((int)mv_off, 1) - mv_off;
+    uint32_t ds_hi, off_hi, eo_hi, to_hi, mv_doc = 0;
+    if constexpr (LIST) {
+        mv_doc = di;
+        ds_hi = sb.doc_srcs[di + 1];
+        off_hi = dst.offsets[di + 1];
+        eo_hi = sb.entry_off[ds_hi];
+        to_hi = tombs ? sb.tomb_off[ds_hi] : 0u;
+    } else {
+        ds_hi = (uint32_t)__shfl_down((int)mv_ds, 1);
+        off_hi = (uint32_t)__shfl_down((int)mv_off, 1);
+        eo_hi = (uint32_t)__shfl_down((int)mv_eo, 1);
+        to_hi = (uint32_t)__shfl_down((int)mv_to, 1);
+    }
+    const uint32_t slots_i = off_hi - mv_off;
     uint32_t n_i = dst.counts ? mv_cnt : slots_i;
     if (lane < cnt && n_i > slots_i) {  // live count beyond the slots: clamped, reported
         err |= kErrCapacity;
         n_i = slots_i;
     }
-    const uint32_t ms_i = (uint32_t)__shfl_down((int)mv_ds, 1) - mv_ds;
-    const uint32_t E_i = (uint32_t)__shfl_down((int)mv_eo, 1) - mv_eo;
-    const uint32_t X_i = (uint32_t)__shfl_down((int)mv_to, 1) - mv_to;
+    const uint32_t ms_i = ds_hi - mv_ds;
+    const uint32_t E_i = eo_hi - mv_eo;
+    const uint32_t X_i = to_hi - mv_to;
     const bool big_i = lane < cnt && ((uint64_t)n_i + E_i + X_i > (uint64_t)Smem::NCAP ||
                                       ms_i > (uint32_t)Smem::MCAP || ms_i * R > (uint32_t)Smem::VCAP);
     const uint64_t bigm = ballot(big_i);
-    if (big_i) push_work(wk, first + lane, n_docs);
-    {   // output slot bounds of the run's documents (+ the batch end after the last one)
+    if (big_i) {
+        if (LEAN)
+            push_defer(wk, first + lane, n_docs);
+        else
+            push_work(wk, di, n_docs);
+    }
+    if (!LIST) {  // output slot bounds of the run's documents (+ the batch end after the last one)
         const bool wr = lane < cnt || (lane == cnt && first + cnt == n_docs);
         st32(mv_off + mv_eo, make_rsrc(out.offsets + first, (cnt + 1u) * 4u), wr ? lane * 4u : kOOB);
     }
@@ -704,18 +738,30 @@ __global__ __launch_bounds__(kFoldWaves * 64) __attribute__((amdgpu_waves_per_eu
     auto rl = [](uint32_t v, uint32_t i) { return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)i); };
     auto meta = [&](uint32_t k) {
         DocMeta q;
-        q.d = first + k;
-        // bounds of lanes k and k + 1 (lane cnt holds the run's end): only the
-        // base vectors stay live through the loop, not their differences
-        q.doff = rl(mv_off, k);
-        q.slots = rl(mv_off, k + 1) - q.doff;
+        if constexpr (LIST) {
+            q.d = rl(mv_doc, k);
+            q.doff = rl(mv_off, k);
+            q.slots = rl(off_hi, k) - q.doff;
+            q.s0 = rl(mv_ds, k);
+            q.ms = rl(ds_hi, k) - q.s0;
+            q.e0 = rl(mv_eo, k);
+            q.E = rl(eo_hi, k) - q.e0;
+            q.t0 = rl(mv_to, k);
+            q.X = rl(to_hi, k) - q.t0;
+        } else {
+            q.d = first + k;
+            // bounds of lanes k and k + 1 (lane cnt holds the run's end): only the
+            // base vectors stay live through the loop, not their differences
+            q.doff = rl(mv_off, k);
+            q.slots = rl(mv_off, k + 1) - q.doff;
+            q.s0 = rl(mv_ds, k);
+            q.ms = rl(mv_ds, k + 1) - q.s0;
+            q.e0 = rl(mv_eo, k);
+            q.E = rl(mv_eo, k + 1) - q.e0;
+            q.t0 = rl(mv_to, k);
+            q.X = rl(mv_to, k + 1) - q.t0;
+        }
         q.n = rl(n_i, k);
-        q.s0 = rl(mv_ds, k);
-        q.ms = rl(mv_ds, k + 1) - q.s0;
-        q.e0 = rl(mv_eo, k);
-        q.E = rl(mv_eo, k + 1) - q.e0;
-        q.t0 = rl(mv_to, k);
-        q.X = rl(mv_to, k + 1) - q.t0;
         q.N = q.n + q.E + q.X;
         q.big = (uint32_t)((bigm >> k) & 1ull);
         return q;
@@ -833,6 +879,7 @@ __global__ __launch_bounds__(kFoldWaves * 64) __attribute__((amdgpu_waves_per_eu
         // ---- fold document k
         uint64_t vfin = 0, full_mask = 0;
         uint32_t U = 0;  // survivors
+        bool deferred = false;  // LEAN: the document is left to the general kernel
         Emit<NCH> em;
         if (!cur.big) {
             const uint32_t n = cur.n, E = cur.E, N = cur.N, ms = cur.ms;
@@ -1015,7 +1062,14 @@ __global__ __launch_bounds__(kFoldWaves * 64) __attribute__((amdgpu_waves_per_eu
             else if constexpr (NCH == 4)
                 walked = dense_delta_walk(m, key, step, isE, isT, flag, full_mask, noop_mask, N, n, ms, R, lane, lt,
                                           em, U STAMP_ARGS);
-            if (!walked) {
+            if (LEAN && !walked) {  // left to the general kernel: nothing written here
+                deferred = true;
+                if (lane == 0) push_defer(wk, cur.d, n_docs);
+#pragma unroll
+                for (int q = 0; q < NCH; ++q) em.off[q] = kOOB;
+                U = 0;
+            }
+            if constexpr (!LEAN) if (!walked) {
             // keep + tag, compacted in place over m.tk (every read of m.tk is done)
             uint32_t Kc = 0;
 #pragma unroll
@@ -1069,8 +1123,9 @@ __global__ __launch_bounds__(kFoldWaves * 64) __attribute__((amdgpu_waves_per_eu
             st64<kAuxNT>(em.c[q], oc, o8);
         }
         const uint32_t carry = U;
-        st32(carry, make_rsrc(out.counts + cur.d, cur.big ? 0u : 4u), lane == 0 ? 0u : kOOB);
-        st64(vfin, make_rsrc(out.vv + (size_t)cur.d * R, cur.big ? 0u : R * 8u), lane * 8u);
+        const bool none = cur.big || deferred;
+        st32(carry, make_rsrc(out.counts + cur.d, none ? 0u : 4u), lane == 0 ? 0u : kOOB);
+        st64(vfin, make_rsrc(out.vv + (size_t)cur.d * R, none ? 0u : R * 8u), lane * 8u);
         wave_sync();
         STAMP(6)
     }
@@ -1169,17 +1224,29 @@ __global__ __launch_bounds__(NT) void fold_block_kernel(int mode, BatchView dst,
 constexpr int kFoldNT = 256;
 constexpr int kFoldIPT = 4;
 
+// lean_first (delta folds): the lean slot-walk pass over every document, then
+// the general kernel over the documents it deferred (grid sized for all of
+// them; runs past the deferred count exit at once); otherwise the general
+// kernel over every document.
 hipError_t launch_fold(int mode, const BatchView& dst, const SrcView& sb, const OutView& out, const Scratch& scr,
-                       const Work& wk, uint32_t block_grid, hipStream_t stream) {
+                       const Work& wk, uint32_t block_grid, bool lean_first, hipStream_t stream) {
     if (dst.n_docs == 0) return hipSuccess;
     const uint32_t per_block = kFoldWaves * kFoldK;
     const uint32_t grid = (dst.n_docs + per_block - 1) / per_block;
-    if (mode == CRDT_FOLD_DELTA)
-        hipLaunchKernelGGL((fold_pipe_kernel<kFoldK, true>), dim3(grid), dim3(kFoldWaves * 64), 0, stream, dst, sb,
-                           out, wk);
-    else
-        hipLaunchKernelGGL((fold_pipe_kernel<kFoldK, false>), dim3(grid), dim3(kFoldWaves * 64), 0, stream, dst, sb,
-                           out, wk);
+    if (mode == CRDT_FOLD_DELTA && lean_first) {
+        hipLaunchKernelGGL((fold_pipe_kernel<kFoldK, true, true, false>), dim3(grid), dim3(kFoldWaves * 64), 0, stream,
+                           dst, sb, out, wk);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL((fold_pipe_kernel<kFoldK, true, false, true>), dim3(grid), dim3(kFoldWaves * 64), 0,
+                           stream, dst, sb, out, wk);
+    } else if (mode == CRDT_FOLD_DELTA) {
+        hipLaunchKernelGGL((fold_pipe_kernel<kFoldK, true, false, false>), dim3(grid), dim3(kFoldWaves * 64), 0,
+                           stream, dst, sb, out, wk);
+    } else {
+        hipLaunchKernelGGL((fold_pipe_kernel<kFoldK, false, false, false>), dim3(grid), dim3(kFoldWaves * 64), 0,
+                           stream, dst, sb, out, wk);
+    }
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL((fold_block_kernel<kFoldNT, kFoldIPT>), dim3(block_grid), dim3(kFoldNT), 0, stream, mode, dst,

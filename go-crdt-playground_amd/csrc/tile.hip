@@ -543,7 +543,11 @@ __global__ __launch_bounds__(NT) void join_tile_pipe_kernel(BatchView A, BatchVi
         if (tid < 64) {
             uint32_t p0 = 0;
             if (g0 < total && !x0.bad && x0.t != 0) {
+#ifdef CRDT_STAMPS
+                p0 = look_back(tw.flags, g0, x0.t, lane, st_acc + 8);
+#else
                 p0 = look_back(tw.flags, g0, x0.t, lane);
+#endif
                 if (lane == 0) flag_store(tw.flags + g0, kFlagInc | (p0 + agg0));
             }
             if (lane == 0) {

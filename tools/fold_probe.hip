@@ -58,7 +58,7 @@ int main(int argc, char** argv) {
     OutView O = make_out(n, R, oslots);
     uint32_t* ws = dalloc<uint32_t>(64);
     CK(hipMemset(ws, 0, 64 * 4));
-    Work wk{ws + 16, ws, ws + 1, dalloc<uint32_t>(n), ws + 8};
+    Work wk{ws + 16, ws, ws + 1, dalloc<uint32_t>(n), ws + 8, dalloc<uint32_t>(n), ws + 2};
     Scratch scr{dalloc<uint64_t>(oslots), dalloc<uint32_t>(oslots), dalloc<uint64_t>(oslots), oslots};
     BatchView dv{n, R, D.offsets, D.counts, D.keys, D.actors, D.counters, D.vv};
     SrcView sv{n, R, S.doc_srcs, S.src_actor, S.vv, S.entry_off, S.keys, S.actors, S.counters,
@@ -77,7 +77,7 @@ int main(int argc, char** argv) {
             CK(hipEventRecord(e0, 0));
         }
         CK(launch_reset_work(ws, 0));
-        CK(launch_fold(mode, dv, sv, O, scr, wk, 512, 0));
+        CK(launch_fold(mode, dv, sv, O, scr, wk, 512, getenv("FOLD_GENERAL") == nullptr, 0));
     }
     CK(hipEventRecord(e1, 0));
     CK(hipDeviceSynchronize());

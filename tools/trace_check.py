@@ -21,9 +21,9 @@ PEAK = 8000.0
 # config -> kernel name prefix of its dominant launch
 KERNELS = {
     "config2": "void crdt::join_wave_kernel<4, 8, 2, true>",
-    "config3": "void crdt::fold_pipe_kernel<32, true>",
+    "config3": "void crdt::fold_pipe_kernel<32, true, true, false>",
     "config4": "void crdt::join_tile_pipe_kernel<256, 4, true, true>",
-    "config5": "void crdt::fold_pipe_kernel<32, false>",
+    "config5": "void crdt::fold_pipe_kernel<32, false, false, false>",
 }
 
 
@@ -52,8 +52,10 @@ def main():
             "trace_mean_ms": mean, "trace_min_ms": min(durs), "trace_max_ms": max(durs),
             "line_launch_ms": roof["launch_ms"], "ratio_line_over_trace": roof["launch_ms"] / mean,
             "frac_line": roof["frac"], "frac_from_trace": b / (mean / 1e3) / 1e9 / PEAK,
-            "note": ("config4's line times the whole exchange call (wave + plan + tile kernels); the trace mean is "
-                     "join_tile_kernel alone" if name == "config4" else ""),
+            "note": {"config4": "config4's line times the whole exchange call (wave + plan + tile kernels); the trace "
+                                "mean is join_tile_pipe_kernel alone",
+                     "config3": "config3's line times the whole fold call (lean pass + the general pass over the "
+                                "deferred documents); the trace mean is the lean pass alone"}.get(name, ""),
         }
     json.dump(out, sys.stdout, indent=1)
     print()
