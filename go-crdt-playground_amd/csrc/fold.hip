@@ -70,16 +70,21 @@ namespace crdt {
 // per SIMD.  A document it cannot walk (key span >= 256, > 15 sources, an
 // actor == len(VV), or beyond its tuple / clock capacity) is deferred, untouched,
 // to the general kernel, which takes the deferred list (LIST) afterwards.
+// The AWSet fold has a lean pass too (dense_awset_walk only).
 #ifndef CRDT_FOLD_LEAN_WPE
 #define CRDT_FOLD_LEAN_WPE 4
 #endif
+#ifndef CRDT_FOLD_AWSET_LEAN_WPE
+#define CRDT_FOLD_AWSET_LEAN_WPE 6
+#endif
 template <bool DELTA, bool LEAN = false>
 struct FoldShape {
-    static constexpr int WPE = LEAN ? CRDT_FOLD_LEAN_WPE : (DELTA ? CRDT_FOLD_DELTA_WPE : CRDT_FOLD_AWSET_WPE);
+    static constexpr int WPE = LEAN ? (DELTA ? CRDT_FOLD_LEAN_WPE : CRDT_FOLD_AWSET_LEAN_WPE)
+                                    : (DELTA ? CRDT_FOLD_DELTA_WPE : CRDT_FOLD_AWSET_WPE);
     static constexpr int NCH = DELTA ? 4 : 2;
-    static constexpr int VCH = LEAN ? 3 : (DELTA ? 4 : 2);
+    static constexpr int VCH = (LEAN && DELTA) ? 3 : (DELTA ? 4 : 2);
     static constexpr int VCAP =
-        LEAN ? 192 : ((DELTA && CRDT_FOLD_DELTA_WPE < 4) ? 256 : (DELTA ? 224 : 128));
+        (LEAN && DELTA) ? 192 : ((DELTA && CRDT_FOLD_DELTA_WPE < 4) ? 256 : (DELTA ? 224 : 128));
 };
 
 template <int VCAP_, int NCAP_>
@@ -502,19 +507,30 @@ __device__ __forceinline__ bool dense_delta_walk(Smem& m, const uint64_t (&key)[
     }
     wave_sync();
     STAMP(9)
+    // every slot's words first, then its last entry's dot (reads issued
+    // unconditionally: a slot without an entry reads a stale index < 256)
+    uint32_t aw[4], dw[4], lt8[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const uint32_t s = q * 64u + lane;
+        aw[q] = addw[s];
+        dw[q] = dropw[s];
+        lt8[q] = last[s];
+    }
+    uint32_t ea[4];
+    uint64_t ec[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        ea[q] = m.ta[lt8[q]];
+        ec[q] = m.tc[lt8[q]];
+    }
     uint32_t base = 0;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
         const uint32_t s = q * 64u + lane;
-        const uint32_t aw = addw[s], dw = dropw[s];
-        const bool P = aw != 0u && (dw >> (31u - (uint32_t)__clz(aw))) == 0u;
-        uint32_t da = 0;
-        uint64_t dc = 0;
-        if (P) {
-            const uint32_t t = last[s];
-            da = m.ta[t];
-            dc = m.tc[t];
-        }
+        const bool P = aw[q] != 0u && (dw[q] >> (31u - (uint32_t)__clz(aw[q]))) == 0u;
+        const uint32_t da = P ? ea[q] : 0u;
+        const uint64_t dc = P ? ec[q] : 0ull;
         const uint64_t pm = ballot(P);
         e.k[q] = kb + s;
         e.a[q] = da;
@@ -1224,7 +1240,7 @@ __global__ __launch_bounds__(NT) void fold_block_kernel(int mode, BatchView dst,
 constexpr int kFoldNT = 256;
 constexpr int kFoldIPT = 4;
 
-// lean_first (delta folds): the lean slot-walk pass over every document, then
+// lean_first: the lean slot-walk pass over every document, then
 // the general kernel over the documents it deferred (grid sized for all of
 // them; runs past the deferred count exit at once); otherwise the general
 // kernel over every document.
@@ -1242,6 +1258,13 @@ hipError_t launch_fold(int mode, const BatchView& dst, const SrcView& sb, const 
                            stream, dst, sb, out, wk);
     } else if (mode == CRDT_FOLD_DELTA) {
         hipLaunchKernelGGL((fold_pipe_kernel<kFoldK, true, false, false>), dim3(grid), dim3(kFoldWaves * 64), 0,
+                           stream, dst, sb, out, wk);
+    } else if (lean_first) {
+        hipLaunchKernelGGL((fold_pipe_kernel<kFoldK, false, true, false>), dim3(grid), dim3(kFoldWaves * 64), 0,
+                           stream, dst, sb, out, wk);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL((fold_pipe_kernel<kFoldK, false, false, true>), dim3(grid), dim3(kFoldWaves * 64), 0,
                            stream, dst, sb, out, wk);
     } else {
         hipLaunchKernelGGL((fold_pipe_kernel<kFoldK, false, false, false>), dim3(grid), dim3(kFoldWaves * 64), 0,

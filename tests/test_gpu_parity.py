@@ -266,6 +266,39 @@ def test_fold_wide_key_spans(eng, mode):
     assert_same(eng.fold(mode, dst, srcs), want, dst.n_docs, R)
 
 
+@pytest.mark.parametrize("lean", [1, 0])
+def test_delta_fold_lean_pass_defers(eng, lean):
+    """Delta folds run a lean slot-walk pass first (fold.hip LEAN) and defer every
+    document it cannot walk to the general kernel: interleaved in one batch,
+    dense documents next to key spans >= 256, 16+ sources, clocks beyond the lean
+    pass's 192 words (R = 16 x 13 sources), tuples beyond 256 (block path) and
+    empty documents -- the same bits as the general kernel alone and the oracle."""
+    rng = random.Random(77)
+    R = 16
+    dsts, per_doc = [], []
+    for d in range(3000):
+        kind = d % 6
+        universe = 200 if kind == 0 else (5000 if kind == 1 else 150)
+        n_src = {0: rng.randint(0, 10), 1: rng.randint(0, 8), 2: 16, 3: 13, 4: 3, 5: 0}[kind]
+        dn = 0 if kind == 5 else (rng.randint(100, 140) if kind == 4 else rng.randint(0, 60))
+        sn = 60 if kind == 4 else rng.randint(0, 8)
+        dsts.append(random_state(rng, R, dn, universe, 9))
+        chain = []
+        for _ in range(n_src):
+            e, vv = random_state(rng, R, sn, universe, 9)
+            t = random_state(rng, R, rng.randint(0, 3), universe, 9)[0]
+            chain.append((rng.randrange(R), vv, e, t))
+        per_doc.append(chain)
+    dst, srcs = batch_of(R, dsts), src_batch_of(R, per_doc)
+    rc, want = oracle.fold(CRDT_FOLD_DELTA, dst, srcs)
+    assert rc == 0
+    try:
+        eng.set_option("fold_lean_first", lean)
+        assert_same(eng.fold(CRDT_FOLD_DELTA, dst, srcs), want, dst.n_docs, R)
+    finally:
+        eng.set_option("fold_lean_first", 1)
+
+
 @pytest.mark.parametrize("mode", [CRDT_FOLD_AWSET, CRDT_FOLD_DELTA])
 def test_fold_panic_parity_per_doc(eng, mode):
     """actor == len(VV) panics exactly where the reference evaluates HasDot on

@@ -23,7 +23,7 @@ KERNELS = {
     "config2": "void crdt::join_wave_kernel<4, 8, 2, true>",
     "config3": "void crdt::fold_pipe_kernel<32, true, true, false>",
     "config4": "void crdt::join_tile_pipe_kernel<256, 4, true, true>",
-    "config5": "void crdt::fold_pipe_kernel<32, false, false, false>",
+    "config5": "void crdt::fold_pipe_kernel<32, false, true, false>",
 }
 
 
@@ -54,7 +54,9 @@ def main():
             "frac_line": roof["frac"], "frac_from_trace": b / (mean / 1e3) / 1e9 / PEAK,
             "note": {"config4": "config4's line times the whole exchange call (wave + plan + tile kernels); the trace "
                                 "mean is join_tile_pipe_kernel alone",
-                     "config3": "config3's line times the whole fold call (lean pass + the general pass over the "
+                     "config3": "the line times the whole fold call (lean pass + the general pass over the "
+                                "deferred documents); the trace mean is the lean pass alone",
+                     "config5": "the line times the whole fold call (lean pass + the general pass over the "
                                 "deferred documents); the trace mean is the lean pass alone"}.get(name, ""),
         }
     json.dump(out, sys.stdout, indent=1)
