@@ -818,8 +818,7 @@ __global__ __launch_bounds__(kFoldWaves * 64) __attribute__((amdgpu_waves_per_eu
         P.act = ld32(make_rsrc(sb.src_actor + q.s0, q.ms * 4u), lane * 4u);
     };
 
-    FoldPref<NCH, VCH> P;
-    P.eo2 = P.to = P.to2 = 0;
+    FoldPref<NCH, VCH> P{};
     {
         const DocMeta q0 = meta(0);
         if (!q0.big) prefetch(P, q0);
@@ -838,6 +837,15 @@ __global__ __launch_bounds__(kFoldWaves * 64) __attribute__((amdgpu_waves_per_eu
         // metadata re-read per document (lane k of the run's vectors), not carried
         // across the fold: fewer scalar registers live through the loop body
         const DocMeta cur = meta(k);
+        // Every prefetch register is consumed here, on every path: its load
+        // (issued one document ago, before the last write-out's stores) is then
+        // known complete, so the next prefetch may overwrite it without a
+        // vmcnt wait -- which, counted in order, would wait out those stores.
+#pragma unroll
+        for (int c = 0; c < NCH; ++c) asm volatile("" ::"v"(P.k[c]), "v"(P.c[c]), "v"(P.a[c]));
+#pragma unroll
+        for (int c = 0; c < VCH; ++c) asm volatile("" ::"v"(P.sv[c]));
+        asm volatile("" ::"v"(P.dv), "v"(P.eo), "v"(P.eo2), "v"(P.to), "v"(P.to2), "v"(P.act));
         // ---- stage document k (its loads were issued one document ago)
         uint64_t vreg = 0;              // lane r < R: V_0[r]
         uint32_t soffv = 0, toffv = 0;  // lane s: end of source s's entries / tombstones
