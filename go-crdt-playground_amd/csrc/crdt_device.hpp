@@ -225,6 +225,14 @@ constexpr uint32_t kOOB = 0x80000000u;  // byte offset past any descriptor
 __device__ __forceinline__ rsrc_t make_rsrc(const void* p, uint32_t bytes) {
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
 }
+// The same from values the compiler cannot prove wave-uniform but that are: the
+// base and size are read from the first lane, so the descriptor is scalar (a
+// divergent descriptor makes the compiler loop over its distinct values).
+__device__ __forceinline__ rsrc_t make_rsrc_u(const void* p, uint32_t bytes) {
+    const uint64_t a = reinterpret_cast<uint64_t>(p);
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a), hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+    return make_rsrc(reinterpret_cast<const void*>(((uint64_t)hi << 32) | lo), __builtin_amdgcn_readfirstlane(bytes));
+}
 __device__ __forceinline__ uint64_t ld64(rsrc_t r, uint32_t off) {
     return __builtin_bit_cast(uint64_t, __builtin_amdgcn_raw_buffer_load_b64(r, (int)off, 0, 0));
 }

@@ -261,7 +261,7 @@ struct TileRegs {
 
 template <int NT, int IPT>
 __device__ __forceinline__ void tile_issue(const BatchView& A, const BatchView& B, const TileGeo& x, uint32_t tid,
-                                           TileRegs<IPT>& r) {
+                                           const void* dummy, TileRegs<IPT>& r) {
     constexpr uint32_t T = NT * IPT;
     const uint32_t n = x.nA + x.nB;
     const bool peek = x.has_next;
@@ -277,28 +277,32 @@ __device__ __forceinline__ void tile_issue(const BatchView& A, const BatchView& 
         const bool inA = !x.bad && p < x.nA;
         const uint32_t pb = p - x.nA;
         const bool inB = !x.bad && !inA && (p < n || (p == n && peek));
-        r.k[q] = inA ? __builtin_nontemporal_load(ak + p) : (inB ? __builtin_nontemporal_load(bk + pb) : 0ull);
-        r.a[q] = inA ? __builtin_nontemporal_load(aa + p) : (inB ? __builtin_nontemporal_load(ba + pb) : 0u);
-        r.c[q] = inA ? __builtin_nontemporal_load(ac + p) : (inB ? __builtin_nontemporal_load(bc + pb) : 0ull);
+        // one load per array for every lane (address selected; `dummy` for none)
+        const uint64_t* kp = inA ? ak + p : (inB ? bk + pb : static_cast<const uint64_t*>(dummy));
+        const uint32_t* ap = inA ? aa + p : (inB ? ba + pb : static_cast<const uint32_t*>(dummy));
+        const uint64_t* cp = inA ? ac + p : (inB ? bc + pb : static_cast<const uint64_t*>(dummy));
+        // (no select on the values: a lane without an element holds a dummy that
+        // nothing reads, and a select here would wait for the load)
+        r.k[q] = __builtin_nontemporal_load(kp);
+        r.a[q] = __builtin_nontemporal_load(ap);
+        r.c[q] = __builtin_nontemporal_load(cp);
     }
-    r.xk = 0;
-    r.xa = 0;
-    r.xc = 0;
-    r.pk = 0;
-    if (tid == NT - 1) {
-        if (n == T && peek) {
-            r.xk = bk[x.nB];
-            r.xa = ba[x.nB];
-            r.xc = bc[x.nB];
-        }
-        if (x.has_prev) r.pk = ak[-1];
-    }
-    r.va = 0;
-    r.vb = 0;
-    if (!x.bad && tid < A.R) {
-        r.va = A.vv[(size_t)x.d * A.R + tid];
-        r.vb = B.vv[(size_t)x.d * A.R + tid];
-    }
+    // the rest unconditionally (a lane with nothing to load reads `dummy`): the
+    // number of loads issued after the runs' is fixed, so the stage's vmcnt
+    // wait is exact and never waits out the stores issued after them
+    const uint64_t* dk = static_cast<const uint64_t*>(dummy);
+    const uint32_t* da = static_cast<const uint32_t*>(dummy);
+    const bool px = tid == NT - 1 && n == T && peek, pp = tid == NT - 1 && x.has_prev;
+    const bool vl = !x.bad && tid < A.R;
+    // (read only where they exist: the peeked element when the tile is full and
+    // has a successor, the key before it when it has a predecessor, the clocks
+    // of a real tile)
+    r.xk = *(px ? bk + x.nB : dk);
+    r.xa = *(px ? ba + x.nB : da);
+    r.xc = *(px ? bc + x.nB : dk);
+    r.pk = *(pp ? ak - 1 : dk);
+    r.va = *(vl ? A.vv + (size_t)x.d * A.R + tid : dk);
+    r.vb = *(vl ? B.vv + (size_t)x.d * A.R + tid : dk);
 }
 
 // Front of a tile: stage its registers in LDS, merge IPT positions per thread
@@ -395,48 +399,52 @@ __device__ __forceinline__ uint32_t tile_front(TileSmem<NT, IPT>& sm, const Tile
     return tile_decide<NT, IPT>(sm, cur, R, tid, err);
 }
 
-template <typename T, bool NTS>
-__device__ __forceinline__ void out_store(T v, T* p) {
-    if (NTS)
-        __builtin_nontemporal_store(v, p);
-    else
-        *p = v;
-}
-
 // Survivors of a staged tile written coalesced at the document's output base +
-// prefix; the last tile writes the count, tile 0 the merged clock.
+// prefix; the last tile writes the count, tile 0 the merged clock.  Every
+// store is issued by every thread (buffer stores; out-of-range offsets where
+// there is nothing to write, and for `none`), so the count of memory operations
+// after the next tile's loads is fixed and the wait for them is exact.
 template <int NT, int IPT, bool EXCH, bool NTS>
-__device__ __forceinline__ void tile_stores(const TileSmem<NT, IPT>& sm, const TileGeo& cur, uint32_t prefix,
-                                            uint32_t agg, uint32_t R, uint32_t tid, const OutView& o1,
-                                            const OutView& o2) {
-    if (cur.bad) return;
-    const size_t obase = (size_t)cur.obase + prefix;
+__device__ __forceinline__ void tile_stores(const TileSmem<NT, IPT>& sm, const TileGeo& cur, bool none,
+                                            uint32_t prefix, uint32_t agg, uint32_t R, uint32_t tid,
+                                            const OutView& o1, const OutView& o2) {
+    constexpr int AUX = NTS ? kAuxNT : 0;
+    // descriptors from wave-uniform values (a divergent descriptor would make
+    // the compiler loop over its distinct values around every store)
+    const bool w = !none && !cur.bad;
+    const size_t obase = (size_t)uniform(cur.obase + prefix);
+    const uint32_t nb = uniform(w ? agg : 0u);
+    const uint32_t d = uniform(cur.d);
+    const rsrc_t k1 = make_rsrc_u(o1.keys + obase, nb * 8u), a1 = make_rsrc_u(o1.actors + obase, nb * 4u),
+                 c1 = make_rsrc_u(o1.counters + obase, nb * 8u);
+    const rsrc_t k2 = make_rsrc_u(o2.keys + obase, EXCH ? nb * 8u : 0u),
+                 a2 = make_rsrc_u(o2.actors + obase, EXCH ? nb * 4u : 0u),
+                 c2 = make_rsrc_u(o2.counters + obase, EXCH ? nb * 8u : 0u);
 #pragma unroll
     for (int q = 0; q < IPT; ++q) {
         const uint32_t p = tid + q * NT;
-        if (p < agg) {
-            const uint32_t v = sm.stage[p];
-            const uint32_t x1 = v & 0xFFFFu, x2 = v >> 16;
-            const uint64_t key = sm.key[x1];
-            out_store<uint64_t, NTS>(key, o1.keys + obase + p);
-            out_store<uint32_t, NTS>(sm.act[x1], o1.actors + obase + p);
-            out_store<uint64_t, NTS>(sm.ctr[x1], o1.counters + obase + p);
-            if (EXCH) {
-                out_store<uint64_t, NTS>(key, o2.keys + obase + p);
-                out_store<uint32_t, NTS>(sm.act[x2], o2.actors + obase + p);
-                out_store<uint64_t, NTS>(sm.ctr[x2], o2.counters + obase + p);
-            }
+        const bool in = p < nb;
+        const uint32_t v = sm.stage[in ? p : 0u];
+        const uint32_t x1 = in ? (v & 0xFFFFu) : 0u, x2 = in ? (v >> 16) : 0u;
+        const uint64_t key = sm.key[x1];
+        const uint32_t o8 = in ? p * 8u : kOOB, o4 = in ? p * 4u : kOOB;
+        st64<AUX>(key, k1, o8);
+        st32<AUX>(sm.act[x1], a1, o4);
+        st64<AUX>(sm.ctr[x1], c1, o8);
+        if (EXCH) {
+            st64<AUX>(key, k2, o8);
+            st32<AUX>(sm.act[x2], a2, o4);
+            st64<AUX>(sm.ctr[x2], c2, o8);
         }
     }
-    if (cur.last && tid == 0) {
-        o1.counts[cur.d] = prefix + agg;
-        if (EXCH) o2.counts[cur.d] = prefix + agg;
-    }
-    if (cur.t == 0 && tid < R) {  // awset.go:160 -> crdt-misc.go:43-55, the same max both ways
-        const uint64_t m = max(sm.va[tid], sm.vb[tid]);
-        o1.vv[(size_t)cur.d * R + tid] = m;
-        if (EXCH) o2.vv[(size_t)cur.d * R + tid] = m;
-    }
+    const uint32_t co = (w && cur.last && tid == 0) ? 0u : kOOB;
+    st32(prefix + agg, make_rsrc_u(o1.counts + d, 4u), co);
+    if (EXCH) st32(prefix + agg, make_rsrc_u(o2.counts + d, 4u), co);
+    // awset.go:160 -> crdt-misc.go:43-55, the same max both ways
+    const uint64_t m = max(sm.va[tid < R ? tid : 0u], sm.vb[tid < R ? tid : 0u]);
+    const uint32_t vo = (w && cur.t == 0 && tid < R) ? tid * 8u : kOOB;
+    st64(m, make_rsrc_u(o1.vv + (size_t)d * R, R * 8u), vo);
+    if (EXCH) st64(m, make_rsrc_u(o2.vv + (size_t)d * R, R * 8u), vo);
 }
 
 // Persistent workgroups take tiles in order from an atomic dispenser.  The
@@ -459,10 +467,10 @@ __global__ __launch_bounds__(NT) void join_tile_kernel(BatchView A, BatchView B,
     __syncthreads();
     uint32_t g = sm.word[0];
     TileGeo x{};
-    if (g < total) {
-        x = tile_geo(A, tw, g);
-        tile_issue<NT, IPT>(A, B, x, tid, rg);
-    }
+    if (g < total) x = tile_geo(A, tw, g);
+    else x.bad = true;
+    tile_issue<NT, IPT>(A, B, x, tid, tw.desc, rg);
+    tile_stores<NT, IPT, EXCH, NTS>(sm, x, true, 0u, 0u, R, tid, o1, o2);  // (as in the pipelined kernel)
     while (g < total) {
         const TileGeo cur = x;
         const uint32_t agg = tile_front<NT, IPT>(sm, cur, rg, R, tid, err);
@@ -493,12 +501,13 @@ __global__ __launch_bounds__(NT) void join_tile_kernel(BatchView A, BatchView B,
         STAMP(3)
         const uint32_t prefix = sm.word[1];
         const uint32_t gn = sm.word[0];
-        if (gn < total) {  // the next tile's loads overlap this tile's stores
-            x = tile_geo(A, tw, gn);
-            tile_issue<NT, IPT>(A, B, x, tid, rg);
-        }
+        // the next tile's loads overlap this tile's stores (past the end: dummy
+        // loads, so their number never depends on the path)
+        if (gn < total) x = tile_geo(A, tw, gn);
+        else x = TileGeo{}, x.bad = true;
+        tile_issue<NT, IPT>(A, B, x, tid, tw.desc, rg);
         STAMP(4)
-        tile_stores<NT, IPT, EXCH, NTS>(sm, cur, prefix, agg, R, tid, o1, o2);
+        tile_stores<NT, IPT, EXCH, NTS>(sm, cur, false, prefix, agg, R, tid, o1, o2);
         __syncthreads();
         STAMP(5)
         g = gn;
@@ -534,7 +543,11 @@ __global__ __launch_bounds__(NT) void join_tile_pipe_kernel(BatchView A, BatchVi
     uint32_t g1 = word[0];
     if (g1 >= total) return;
     TileGeo x1 = tile_geo(A, tw, g1);
-    tile_issue<NT, IPT>(A, B, x1, tid, rg);
+    tile_issue<NT, IPT>(A, B, x1, tid, tw.desc, rg);
+    // as many (dropped) stores as a round issues after its loads: the loop is
+    // entered with the same memory operations behind them on both paths, so the
+    // stage's wait for them is an exact vmcnt
+    tile_stores<NT, IPT, EXCH, NTS>(sm[1], x1, true, 0u, 0u, R, tid, o1, o2);
     uint32_t g0 = total, agg0 = 0;  // g0 >= total: no tile waiting for its stores
     TileGeo x0{};
     uint32_t buf = 0;
@@ -580,12 +593,13 @@ __global__ __launch_bounds__(NT) void join_tile_pipe_kernel(BatchView A, BatchVi
         resolve0(prefix0, g2);
         STAMP(3)
         TileGeo x2{};
-        if (g2 < total) {  // g2's loads overlap g0's stores
-            x2 = tile_geo(A, tw, g2);
-            tile_issue<NT, IPT>(A, B, x2, tid, rg);
-        }
+        // g2's loads overlap g0's stores; issued even past the end (a tile marked
+        // bad: dummy loads only), so their number never depends on the path
+        if (g2 < total) x2 = tile_geo(A, tw, g2);
+        else x2.bad = true;
+        tile_issue<NT, IPT>(A, B, x2, tid, tw.desc, rg);
         STAMP(4)
-        if (have0) tile_stores<NT, IPT, EXCH, NTS>(sm[buf ^ 1], x0, prefix0, agg0, R, tid, o1, o2);
+        tile_stores<NT, IPT, EXCH, NTS>(sm[buf ^ 1], x0, !have0, prefix0, agg0, R, tid, o1, o2);
         if (!have1 && g2 >= total) break;  // (g2 >= total whenever g1 is: the dispenser only grows)
         __syncthreads();
         STAMP(5)

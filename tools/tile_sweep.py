@@ -31,7 +31,7 @@ def main():
     a, b = A.as_batch(), B.as_batch()
     ref = None
     shapes = [tuple(int(v) for v in a.split(":")) for a in sys.argv[2:]] or \
-        [(2, 1), (4, 1), (8, 1), (5, 1), (9, 1), (8, 0), (4, 1), (8, 1), (2, 1)]
+        [(2, 1), (4, 1), (4, 0), (5, 1), (6, 1), (7, 1), (1, 1), (4, 1), (2, 1)]
     for shape, nts in shapes:
         eng.set_option("join_tile_shape", shape)
         eng.set_option("join_tile_nt_stores", nts)
