@@ -157,6 +157,7 @@ int crdt_ctx_set_max_doc_entries(crdt_ctx* ctx, uint32_t max_entries);
  *   "join_docs_per_wave"  1|2|4|8|16  documents one wavefront pipelines (default 8)
  *   "join_nt_stores"      0|1         non-temporal output stores (default 1)
  *   "probe_blocks_per_cu" 1..64       crdt_bw_probe grid (default 16)
+ *   "fold_lean_first"     0|1         folds: slot-walk pass first, the rest deferred (default 1)
  *   (also "join_tile_capacity", "join_tile_shape", "join_tile_nt_stores",
  *   "join_tiles": see api.cpp)
  * and one layout option of the host-buffer (*_batch) joins, exchanges and folds:
