@@ -286,7 +286,8 @@ class Config4(Config2):
     @property
     def kernel_name(self):
         return ("join_tile_pipe_kernel (exchange call: join_wave_kernel for docs <= 64 per side, tile plan, merge-path "
-                "tiles of 1024 positions placed by a look-back deferred by one tile; timed as the whole call)")
+                "tiles of 1024 positions placed by a look-back deferred by one tile, stores in aligned 64-slot windows; "
+                "timed as the whole call)")
 
     def describe(self, world):
         return {"workload": "config4: %d docs/GPU, Zipf(1.1)-like sizes in [1, 2^20) (mean %.0f, max %d, %d entries "

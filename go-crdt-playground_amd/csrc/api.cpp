@@ -119,7 +119,7 @@ struct crdt_ctx {
     DevBuf sort_tmp, sort_idx, sort_ends;  // ingest sort (sort.hip)
     uint32_t tile_cap = 1u << 20;             // crdt_ctx_set_option("join_tile_capacity")
     bool join_tiles = true;                   // crdt_ctx_set_option("join_tiles")
-    uint32_t tile_shape = 5;                  // crdt_ctx_set_option("join_tile_shape")
+    uint32_t tile_shape = 9;                  // crdt_ctx_set_option("join_tile_shape")
     bool tile_nt_stores = true;               // crdt_ctx_set_option("join_tile_nt_stores")
     size_t scratch_slots = 0;
     uint32_t max_doc_entries = 0xFFFFFFFFu;  // caller's promise (crdt_ctx_set_max_doc_entries)
@@ -345,8 +345,9 @@ int crdt_ctx_set_option(crdt_ctx* ctx, const char* name, int64_t value) {
         return CRDT_OK;
     }
     if (!strcmp(name, "join_tile_shape")) {  // threads x positions: look-back per tile 0: 512x4, 1: 256x4, 2: 256x8,
-                                             // 3: 1024x2; deferred by a tile 4: 256x4, 5: 512x2 (default), 6: 256x8, 7: 128x8
-        if (value < 0 || value > 7) return CRDT_E_INVALID;
+                                             // 3: 1024x2; deferred by a tile 4: 256x4, 5: 512x2, 6: 256x8, 7: 128x8,
+                                             // and aligned store windows 8: 256x4, 9: 512x2 (default)
+        if (value < 0 || value > 9) return CRDT_E_INVALID;
         ctx->tile_shape = (uint32_t)value;
         return CRDT_OK;
     }

@@ -679,6 +679,10 @@ struct DocMeta {
 };
 
 constexpr int kFoldWaves = 2;  // wavefronts per workgroup (independent)
+#ifndef CRDT_FOLD_STORE_AUX
+#define CRDT_FOLD_STORE_AUX 2  // survivors' cache policy: 2 = non-temporal, 0 = plain
+#endif
+constexpr int kFoldStoreAux = CRDT_FOLD_STORE_AUX;
 constexpr int kFoldK = 32;     // consecutive documents per wavefront
 // stores of one document's write-out: walk rounds x 3 + count + VV
 __host__ __device__ constexpr int fold_stores(int nch) { return nch * 3 + 2; }
@@ -1142,9 +1146,9 @@ __global__ __launch_bounds__(kFoldWaves * 64) __attribute__((amdgpu_waves_per_eu
         for (int q = 0; q < NCH; ++q) {
             const uint32_t o = em.off[q];
             const uint32_t o8 = o == kOOB ? kOOB : o * 8u, o4 = o == kOOB ? kOOB : o * 4u;
-            st64<kAuxNT>(em.k[q], ok, o8);
-            st32<kAuxNT>(em.a[q], oa, o4);
-            st64<kAuxNT>(em.c[q], oc, o8);
+            st64<kFoldStoreAux>(em.k[q], ok, o8);
+            st32<kFoldStoreAux>(em.a[q], oa, o4);
+            st64<kFoldStoreAux>(em.c[q], oc, o8);
         }
         const uint32_t carry = U;
         const bool none = cur.big || deferred;

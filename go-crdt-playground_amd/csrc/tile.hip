@@ -404,7 +404,12 @@ __device__ __forceinline__ uint32_t tile_front(TileSmem<NT, IPT>& sm, const Tile
 // store is issued by every thread (buffer stores; out-of-range offsets where
 // there is nothing to write, and for `none`), so the count of memory operations
 // after the next tile's loads is fixed and the wait for them is exact.
-template <int NT, int IPT, bool EXCH, bool NTS>
+//
+// ALIGN: lane l of every store instruction writes an output slot = l (mod 64),
+// so each wave-instruction covers one aligned 64-slot window (whole cache
+// lines; the tile's first and last windows are shared with its neighbours);
+// one more round of stores than positions per thread.
+template <int NT, int IPT, bool EXCH, bool NTS, bool ALIGN = false>
 __device__ __forceinline__ void tile_stores(const TileSmem<NT, IPT>& sm, const TileGeo& cur, bool none,
                                             uint32_t prefix, uint32_t agg, uint32_t R, uint32_t tid,
                                             const OutView& o1, const OutView& o2) {
@@ -420,9 +425,10 @@ __device__ __forceinline__ void tile_stores(const TileSmem<NT, IPT>& sm, const T
     const rsrc_t k2 = make_rsrc_u(o2.keys + obase, EXCH ? nb * 8u : 0u),
                  a2 = make_rsrc_u(o2.actors + obase, EXCH ? nb * 4u : 0u),
                  c2 = make_rsrc_u(o2.counters + obase, EXCH ? nb * 8u : 0u);
+    const uint32_t shift = ALIGN ? (uint32_t)(obase & 63u) : 0u;
 #pragma unroll
-    for (int q = 0; q < IPT; ++q) {
-        const uint32_t p = tid + q * NT;
+    for (int q = 0; q < IPT + (ALIGN ? 1 : 0); ++q) {
+        const uint32_t p = tid + q * NT - shift;  // wraps below 0: out of range
         const bool in = p < nb;
         const uint32_t v = sm.stage[in ? p : 0u];
         const uint32_t x1 = in ? (v & 0xFFFFu) : 0u, x2 = in ? (v >> 16) : 0u;
@@ -526,7 +532,7 @@ __global__ __launch_bounds__(NT) void join_tile_kernel(BatchView A, BatchView B,
 // look-back and decided next round with nothing to wait on in between -- so
 // every walk ends (each tile's aggregate is published without waiting, and
 // tile 0 of a document publishes its inclusive count).
-template <int NT, int IPT, bool EXCH, bool NTS>
+template <int NT, int IPT, bool EXCH, bool NTS, bool ALIGN>
 __global__ __launch_bounds__(NT) void join_tile_pipe_kernel(BatchView A, BatchView B, OutView o1, OutView o2,
                                                             TileWork tw, Work wk) {
     __shared__ TileSmem<NT, IPT> sm[2];
@@ -547,7 +553,7 @@ __global__ __launch_bounds__(NT) void join_tile_pipe_kernel(BatchView A, BatchVi
     // as many (dropped) stores as a round issues after its loads: the loop is
     // entered with the same memory operations behind them on both paths, so the
     // stage's wait for them is an exact vmcnt
-    tile_stores<NT, IPT, EXCH, NTS>(sm[1], x1, true, 0u, 0u, R, tid, o1, o2);
+    tile_stores<NT, IPT, EXCH, NTS, ALIGN>(sm[1], x1, true, 0u, 0u, R, tid, o1, o2);
     uint32_t g0 = total, agg0 = 0;  // g0 >= total: no tile waiting for its stores
     TileGeo x0{};
     uint32_t buf = 0;
@@ -599,7 +605,7 @@ __global__ __launch_bounds__(NT) void join_tile_pipe_kernel(BatchView A, BatchVi
         else x2.bad = true;
         tile_issue<NT, IPT>(A, B, x2, tid, tw.desc, rg);
         STAMP(4)
-        tile_stores<NT, IPT, EXCH, NTS>(sm[buf ^ 1], x0, !have0, prefix0, agg0, R, tid, o1, o2);
+        tile_stores<NT, IPT, EXCH, NTS, ALIGN>(sm[buf ^ 1], x0, !have0, prefix0, agg0, R, tid, o1, o2);
         if (!have1 && g2 >= total) break;  // (g2 >= total whenever g1 is: the dispenser only grows)
         __syncthreads();
         STAMP(5)
@@ -637,13 +643,13 @@ static hipError_t launch_tile_kernel_s(const BatchView& A, const BatchView& B, c
     return hipGetLastError();
 }
 
-template <int NT, int IPT, bool NTS>
+template <int NT, int IPT, bool NTS, bool ALIGN>
 static hipError_t launch_tile_pipe_s(const BatchView& A, const BatchView& B, const OutView& o1, const OutView* o2,
                                      const Work& wk, const TileWork& tw, uint32_t n_cu, hipStream_t stream) {
     static int per_cu = 0;  // resident workgroups per CU (occupancy query, once per shape)
     if (per_cu == 0) {
         int nb = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, join_tile_pipe_kernel<NT, IPT, true, NTS>, NT, 0) !=
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, join_tile_pipe_kernel<NT, IPT, true, NTS, ALIGN>, NT, 0) !=
                 hipSuccess ||
             nb < 1)
             nb = 1;
@@ -651,19 +657,19 @@ static hipError_t launch_tile_pipe_s(const BatchView& A, const BatchView& B, con
     }
     const dim3 grid(n_cu * per_cu);
     if (o2)
-        hipLaunchKernelGGL((join_tile_pipe_kernel<NT, IPT, true, NTS>), grid, dim3(NT), 0, stream, A, B, o1, *o2, tw,
+        hipLaunchKernelGGL((join_tile_pipe_kernel<NT, IPT, true, NTS, ALIGN>), grid, dim3(NT), 0, stream, A, B, o1, *o2, tw,
                            wk);
     else
-        hipLaunchKernelGGL((join_tile_pipe_kernel<NT, IPT, false, NTS>), grid, dim3(NT), 0, stream, A, B, o1, o1, tw,
+        hipLaunchKernelGGL((join_tile_pipe_kernel<NT, IPT, false, NTS, ALIGN>), grid, dim3(NT), 0, stream, A, B, o1, o1, tw,
                            wk);
     return hipGetLastError();
 }
 
-template <int NT, int IPT>
+template <int NT, int IPT, bool ALIGN = false>
 static hipError_t launch_tile_pipe(const BatchView& A, const BatchView& B, const OutView& o1, const OutView* o2,
                                    const Work& wk, const TileWork& tw, uint32_t n_cu, hipStream_t stream) {
-    return tw.nt_stores ? launch_tile_pipe_s<NT, IPT, true>(A, B, o1, o2, wk, tw, n_cu, stream)
-                        : launch_tile_pipe_s<NT, IPT, false>(A, B, o1, o2, wk, tw, n_cu, stream);
+    return tw.nt_stores ? launch_tile_pipe_s<NT, IPT, true, ALIGN>(A, B, o1, o2, wk, tw, n_cu, stream)
+                        : launch_tile_pipe_s<NT, IPT, false, ALIGN>(A, B, o1, o2, wk, tw, n_cu, stream);
 }
 
 template <int NT, int IPT>
@@ -682,6 +688,8 @@ uint32_t tile_positions(uint32_t shape) {
         case 5: return 512 * 2;
         case 6: return 256 * 8;
         case 7: return 128 * 8;
+        case 8: return 256 * 4;  // aligned store windows
+        case 9: return 512 * 2;
         default: return 512 * 4;
     }
 }
@@ -711,6 +719,8 @@ hipError_t launch_join_tiles(const BatchView& A, const BatchView& B, const OutVi
         case 5: return launch_tile_pipe<512, 2>(A, B, o1, o2, wk, tw, n_cu, stream);
         case 6: return launch_tile_pipe<256, 8>(A, B, o1, o2, wk, tw, n_cu, stream);
         case 7: return launch_tile_pipe<128, 8>(A, B, o1, o2, wk, tw, n_cu, stream);
+        case 8: return launch_tile_pipe<256, 4, true>(A, B, o1, o2, wk, tw, n_cu, stream);
+        case 9: return launch_tile_pipe<512, 2, true>(A, B, o1, o2, wk, tw, n_cu, stream);
         default: return launch_tile_kernel<512, 4>(A, B, o1, o2, wk, tw, n_cu, stream);
     }
 }
