@@ -63,12 +63,19 @@ __device__ __forceinline__ void lanes_issue(JoinLanes& L, const BatchView& dst, 
                                             const JoinMeta& m, uint32_t d, bool ld, uint32_t lane, uint32_t R) {
     const uint32_t dn = ld ? m.dn : 0u, sn = ld ? m.sn : 0u, rv = ld ? R : 0u;
     const uint32_t o8 = lane * 8u, o4 = lane * 4u;
-    L.dk = ld64(make_rsrc(dst.keys + m.doff, dn * 8u), o8);
-    L.da = ld32(make_rsrc(dst.actors + m.doff, dn * 4u), o4);
-    L.dc = ld64(make_rsrc(dst.counters + m.doff, dn * 8u), o8);
-    L.sk = ld64(make_rsrc(src.keys + m.soff, sn * 8u), o8);
-    L.sa = ld32(make_rsrc(src.actors + m.soff, sn * 4u), o4);
-    L.sc = ld64(make_rsrc(src.counters + m.soff, sn * 8u), o8);
+    // non-temporal entry loads: each entry is read once (1.3 % faster than the
+    // default policy, and than aux 1 / 3, measured on one box)
+    constexpr int LA = kAuxNT;
+    auto l64 = [](rsrc_t r, uint32_t off) {
+        return __builtin_bit_cast(uint64_t, __builtin_amdgcn_raw_buffer_load_b64(r, (int)off, 0, LA));
+    };
+    auto l32 = [](rsrc_t r, uint32_t off) { return (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(r, (int)off, 0, LA); };
+    L.dk = l64(make_rsrc(dst.keys + m.doff, dn * 8u), o8);
+    L.da = l32(make_rsrc(dst.actors + m.doff, dn * 4u), o4);
+    L.dc = l64(make_rsrc(dst.counters + m.doff, dn * 8u), o8);
+    L.sk = l64(make_rsrc(src.keys + m.soff, sn * 8u), o8);
+    L.sa = l32(make_rsrc(src.actors + m.soff, sn * 4u), o4);
+    L.sc = l64(make_rsrc(src.counters + m.soff, sn * 8u), o8);
     const size_t vo = ld ? (size_t)d * R : 0;
     L.vd = ld64(make_rsrc(dst.vv + vo, rv * 8u), o8);
     L.vs = ld64(make_rsrc(src.vv + vo, rv * 8u), o8);
