@@ -758,6 +758,20 @@ int crdt_validate_tomb_batch(const crdt_tomb_batch* t, uint32_t n_docs) {
 
 namespace {
 
+// Diagnostics (CRDT_TRACE_STAGE): host time between the phases of a batch call.
+struct PhaseClock {
+    const char* what;
+    bool on = std::getenv("CRDT_TRACE_STAGE") != nullptr;
+    std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
+    explicit PhaseClock(const char* w) : what(w) {}
+    void mark(const char* phase) {
+        if (!on) return;
+        const auto n = std::chrono::steady_clock::now();
+        fprintf(stderr, "%s: %s %.3f ms\n", what, phase, std::chrono::duration<double, std::milli>(n - t).count());
+        t = n;
+    }
+};
+
 struct Stager {
     crdt_ctx* ctx;
     int next = 0;
@@ -968,18 +982,24 @@ int crdt_awset_exchange_batch(crdt_ctx* ctx, const crdt_awset_batch* a, const cr
     if (a->n_docs != b->n_docs || a->R != b->R) return CRDT_E_INVALID;
     if ((uint64_t)a->offsets[a->n_docs] + b->offsets[b->n_docs] >= (1ull << 32)) return CRDT_E_INVALID;
     if ((rc = set_device(ctx)) != CRDT_OK) return rc;
+    PhaseClock pc("exchange_batch");
     Stager st{ctx};
     crdt_awset_batch da = stage_batch(st, a), db = stage_batch(st, b);
     const size_t slots = (size_t)a->offsets[a->n_docs] + b->offsets[b->n_docs];
     crdt_awset_out o1 = stage_out(st, a->n_docs, a->R, slots);
     crdt_awset_out o2 = stage_out(st, a->n_docs, a->R, slots);
     if (st.rc != CRDT_OK) return st.rc;
+    pc.mark("stage issued");
     rc = check_order(ctx, da.offsets, da.counts, da.n_docs, da.keys);
     if (rc == CRDT_OK) rc = check_order(ctx, db.offsets, db.counts, db.n_docs, db.keys);
     if (rc == CRDT_OK) rc = crdt_awset_exchange_async(ctx, &da, &db, &o1, &o2, ctx->stream);
+    pc.mark("kernels issued");
     if (rc == CRDT_OK) rc = fetch_merge_out(ctx, st, out_ab, o1, a->n_docs, a->R, slots);
+    pc.mark("fetch a<-b issued (after a sync)");
     if (rc == CRDT_OK) rc = fetch_merge_out(ctx, st, out_ba, o2, a->n_docs, a->R, slots);
+    pc.mark("fetch b<-a issued (after a sync)");
     const int sync = crdt_ctx_sync(ctx, ctx->stream);
+    pc.mark("synced");
     return rc != CRDT_OK ? rc : sync;
 }
 
