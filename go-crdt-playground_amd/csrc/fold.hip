@@ -687,7 +687,15 @@ struct DocMeta {
 #ifndef CRDT_FOLD_K_DELTA
 #define CRDT_FOLD_K_DELTA 16
 #endif
-constexpr int kFoldWaves = CRDT_FOLD_WAVES;  // wavefronts per workgroup (independent)
+#ifndef CRDT_FOLD_WAVES_DELTA
+#define CRDT_FOLD_WAVES_DELTA 1
+#endif
+// wavefronts per workgroup (independent): AWSet folds 2; delta folds 1 (2 %
+// faster than 2 on config 3, measured; the AWSet fold is the same either way)
+constexpr int kFoldWaves = CRDT_FOLD_WAVES;
+constexpr int kFoldWavesD = CRDT_FOLD_WAVES_DELTA;
+template <bool DELTA>
+constexpr int fold_waves() { return DELTA ? kFoldWavesD : kFoldWaves; }
 // survivors' stores: non-temporal (plain stores measured no faster)
 constexpr int kFoldStoreAux = kAuxNT;
 constexpr int kFoldK = CRDT_FOLD_K;  // consecutive documents per wavefront (AWSet folds)
@@ -696,12 +704,12 @@ constexpr int kFoldKD = CRDT_FOLD_K_DELTA;  // (delta folds: 16, measured 2 % fa
 __host__ __device__ constexpr int fold_stores(int nch) { return nch * 3 + 2; }
 
 template <int K, bool DELTA, bool LEAN, bool LIST>
-__global__ __launch_bounds__(kFoldWaves * 64) __attribute__((amdgpu_waves_per_eu(FoldShape<DELTA, LEAN>::WPE))) void fold_pipe_kernel(BatchView dst, SrcView sb, OutView out, Work wk) {
+__global__ __launch_bounds__(fold_waves<DELTA>() * 64) __attribute__((amdgpu_waves_per_eu(FoldShape<DELTA, LEAN>::WPE))) void fold_pipe_kernel(BatchView dst, SrcView sb, OutView out, Work wk) {
     static_assert(!(LEAN && LIST), "the lean pass runs over consecutive documents");
     static_assert(K >= 1 && K < 64, "a run's end bounds live in lane K: K < 64");
     constexpr int NCH = FoldShape<DELTA, LEAN>::NCH, VCH = FoldShape<DELTA, LEAN>::VCH;
     using Smem = FoldSmem<FoldShape<DELTA, LEAN>::VCAP, 64 * NCH>;
-    __shared__ Smem smem[kFoldWaves];
+    __shared__ Smem smem[fold_waves<DELTA>()];
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t w = threadIdx.x >> 6;
     Smem& m = smem[w];
@@ -716,7 +724,7 @@ __global__ __launch_bounds__(kFoldWaves * 64) __attribute__((amdgpu_waves_per_eu
     const uint32_t n_run = LIST ? min(__hip_atomic_load(wk.defer_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
                                       n_docs)
                                 : n_docs;
-    const uint32_t first = uniform((blockIdx.x * kFoldWaves + w) * (uint32_t)K);
+    const uint32_t first = uniform((blockIdx.x * fold_waves<DELTA>() + w) * (uint32_t)K);
     if (first >= n_run) return;
     const uint32_t cnt = min((uint32_t)K, n_run - first);
 
@@ -1270,16 +1278,16 @@ hipError_t launch_fold(int mode, const BatchView& dst, const SrcView& sb, const 
                        const Work& wk, uint32_t block_grid, bool lean_first, hipStream_t stream) {
     if (dst.n_docs == 0) return hipSuccess;
     const uint32_t grid = (dst.n_docs + kFoldWaves * kFoldK - 1) / (kFoldWaves * kFoldK);
-    const uint32_t grid_d = (dst.n_docs + kFoldWaves * kFoldKD - 1) / (kFoldWaves * kFoldKD);
+    const uint32_t grid_d = (dst.n_docs + kFoldWavesD * kFoldKD - 1) / (kFoldWavesD * kFoldKD);
     if (mode == CRDT_FOLD_DELTA && lean_first) {
-        hipLaunchKernelGGL((fold_pipe_kernel<kFoldKD, true, true, false>), dim3(grid_d), dim3(kFoldWaves * 64), 0,
+        hipLaunchKernelGGL((fold_pipe_kernel<kFoldKD, true, true, false>), dim3(grid_d), dim3(kFoldWavesD * 64), 0,
                            stream, dst, sb, out, wk);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
-        hipLaunchKernelGGL((fold_pipe_kernel<kFoldKD, true, false, true>), dim3(grid_d), dim3(kFoldWaves * 64), 0,
+        hipLaunchKernelGGL((fold_pipe_kernel<kFoldKD, true, false, true>), dim3(grid_d), dim3(kFoldWavesD * 64), 0,
                            stream, dst, sb, out, wk);
     } else if (mode == CRDT_FOLD_DELTA) {
-        hipLaunchKernelGGL((fold_pipe_kernel<kFoldKD, true, false, false>), dim3(grid_d), dim3(kFoldWaves * 64), 0,
+        hipLaunchKernelGGL((fold_pipe_kernel<kFoldKD, true, false, false>), dim3(grid_d), dim3(kFoldWavesD * 64), 0,
                            stream, dst, sb, out, wk);
     } else if (lean_first) {
         hipLaunchKernelGGL((fold_pipe_kernel<kFoldK, false, true, false>), dim3(grid), dim3(kFoldWaves * 64), 0,
