@@ -691,7 +691,8 @@ int crdt_clock_probe(crdt_ctx* ctx, double* mhz) {
 
 // Pointers, slot bounds, live counts and (keys = true) the key order.  The
 // *_batch calls check only the layout here (O(documents)) and the key order
-// on the device after the upload (pack.hip, check_order_kernel).
+// on the device after the upload (pack.hip, check_order_kernel), whose verdict
+// they read back before launching a merge (order_gate).
 static int validate_batch(const crdt_awset_batch* b, bool keys) {
     if (!b || !b->offsets || b->R == 0 || b->R > CRDT_MAX_R) return CRDT_E_INVALID;
     if (b->n_docs && (!b->vv || ((b->offsets[b->n_docs] > b->offsets[0]) && (!b->keys || !b->actors || !b->counters))))
@@ -847,6 +848,13 @@ int check_order(crdt_ctx* ctx, const uint32_t* off, const uint32_t* cnt, uint32_
     return hip_err(launch_check_order(off, cnt, n, keys, ctx->ws.as<uint32_t>(64), (uint32_t)ctx->n_cu, ctx->stream));
 }
 
+// The order checks' verdict, read back before any merge kernel is launched:
+// the merge kernels assume strictly ascending keys, so a batch that is not
+// never reaches them (one small sync; the uploads precede the merge anyway).
+int order_gate(crdt_ctx* ctx, int rc) {
+    return rc == CRDT_OK ? crdt_ctx_sync(ctx, ctx->stream) : rc;
+}
+
 // Download a merge output: at its capacity offsets, or (pack_batch_outputs)
 // only the live entries, gathered on the device at offsets = the prefix sums
 // of the counts, so PCIe moves live entries only.
@@ -967,6 +975,7 @@ int crdt_awset_join_batch(crdt_ctx* ctx, const crdt_awset_batch* dst, const crdt
     if (st.rc != CRDT_OK) return st.rc;
     rc = check_order(ctx, dd.offsets, dd.counts, dd.n_docs, dd.keys);
     if (rc == CRDT_OK) rc = check_order(ctx, ds.offsets, ds.counts, ds.n_docs, ds.keys);
+    rc = order_gate(ctx, rc);
     if (rc == CRDT_OK) rc = crdt_awset_join_async(ctx, &dd, &ds, &dout, ctx->stream);
     if (rc == CRDT_OK) rc = fetch_merge_out(ctx, st, out, dout, dst->n_docs, dst->R, slots);
     const int sync = crdt_ctx_sync(ctx, ctx->stream);
@@ -992,6 +1001,8 @@ int crdt_awset_exchange_batch(crdt_ctx* ctx, const crdt_awset_batch* a, const cr
     pc.mark("stage issued");
     rc = check_order(ctx, da.offsets, da.counts, da.n_docs, da.keys);
     if (rc == CRDT_OK) rc = check_order(ctx, db.offsets, db.counts, db.n_docs, db.keys);
+    rc = order_gate(ctx, rc);
+    pc.mark("order checked (a sync)");
     if (rc == CRDT_OK) rc = crdt_awset_exchange_async(ctx, &da, &db, &o1, &o2, ctx->stream);
     pc.mark("kernels issued");
     if (rc == CRDT_OK) rc = fetch_merge_out(ctx, st, out_ab, o1, a->n_docs, a->R, slots);
@@ -1038,6 +1049,7 @@ int crdt_awset_fold_batch(crdt_ctx* ctx, int mode, const crdt_awset_batch* dst, 
     rc = check_order(ctx, dd.offsets, dd.counts, dd.n_docs, dd.keys);
     if (rc == CRDT_OK) rc = check_order(ctx, ds.entry_off, nullptr, ns, ds.keys);
     if (rc == CRDT_OK && srcs->tomb_off) rc = check_order(ctx, ds.tomb_off, nullptr, ns, ds.tkeys);
+    rc = order_gate(ctx, rc);
     if (rc == CRDT_OK) rc = crdt_awset_fold_async(ctx, mode, &dd, &ds, &dout, ctx->stream);
     if (rc == CRDT_OK) rc = fetch_merge_out(ctx, st, out, dout, dst->n_docs, dst->R, total);
     const int sync = crdt_ctx_sync(ctx, ctx->stream);

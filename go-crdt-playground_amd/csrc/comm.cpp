@@ -37,6 +37,7 @@ struct Rccl {
     ncclResult_t (*init_rank)(ncclComm_t*, int, ncclUniqueId, int) = nullptr;
     ncclResult_t (*init_all)(ncclComm_t*, int, const int*) = nullptr;
     ncclResult_t (*destroy)(ncclComm_t) = nullptr;
+    ncclResult_t (*abort)(ncclComm_t) = nullptr;
     ncclResult_t (*all_reduce)(const void*, void*, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t,
                                hipStream_t) = nullptr;
     ncclResult_t (*group_start)() = nullptr;
@@ -65,6 +66,7 @@ const Rccl* rccl() {
     r.tried = true;
     if (!bind(h, "ncclGetUniqueId", r.get_unique_id) || !bind(h, "ncclCommInitRank", r.init_rank) ||
         !bind(h, "ncclCommInitAll", r.init_all) || !bind(h, "ncclCommDestroy", r.destroy) ||
+        !bind(h, "ncclCommAbort", r.abort) ||
         !bind(h, "ncclAllReduce", r.all_reduce) || !bind(h, "ncclGroupStart", r.group_start) ||
         !bind(h, "ncclGroupEnd", r.group_end))
         return nullptr;
@@ -77,9 +79,9 @@ struct Group {
     std::vector<crdt_ctx*> members;
 };
 
-void drop_comm(const Rccl* r, crdt_ctx* c) {
+void drop_comm(const Rccl* r, crdt_ctx* c, bool abort = false) {
     void** comm = crdt_internal_comm(c);
-    if (*comm && r) (void)r->destroy((ncclComm_t)*comm);
+    if (*comm && r) (void)(abort ? r->abort : r->destroy)((ncclComm_t)*comm);
     *comm = nullptr;
     void** grp = crdt_internal_comm_group(c);
     if (*grp) {
@@ -188,7 +190,10 @@ int crdt_global_context_allreduce(crdt_ctx* const* per_gpu, int n_gpus, uint64_t
     }
     // A group that was started must be ended even when an enqueue failed (an
     // open group would swallow the caller's next RCCL calls); after the first
-    // failure no further all-reduce is enqueued and the call reports it.
+    // failure no further all-reduce is enqueued. A partly issued collective
+    // would leave the enqueued ranks' streams waiting for the missing ones, so
+    // the communicators are then aborted (their pending work is dropped) and
+    // the group dissolved: the next call builds fresh communicators.
     if (r->group_start() != ncclSuccess) return CRDT_E_RCCL;
     bool ok = true;
     for (int i = 0; i < n_gpus; ++i) {
@@ -196,7 +201,11 @@ int crdt_global_context_allreduce(crdt_ctx* const* per_gpu, int n_gpus, uint64_t
         ok = ok && r->all_reduce(vv_R[i], vv_R[i], R, ncclUint64, ncclMax, (ncclComm_t)*crdt_internal_comm(per_gpu[i]),
                                  crdt_internal_stream(per_gpu[i])) == ncclSuccess;
     }
-    if (r->group_end() != ncclSuccess || !ok) return CRDT_E_RCCL;
+    const bool ended = r->group_end() == ncclSuccess;
+    if (!ok || !ended) {
+        for (int i = 0; i < n_gpus; ++i) drop_comm(r, per_gpu[i], true);
+        return CRDT_E_RCCL;
+    }
     for (int i = 0; i < n_gpus; ++i) {
         if (hipSetDevice(devs[i]) != hipSuccess) return CRDT_E_HIP;
         if (hipStreamSynchronize(crdt_internal_stream(per_gpu[i])) != hipSuccess) return CRDT_E_HIP;

@@ -108,6 +108,17 @@ struct FoldSmem {
     alignas(8) uint16_t dbase[256];  // dense_sort: first sorted position of each key slot (64-bit stores)
 };
 
+// The members reached by 64-bit LDS accesses (atomics on stag, stores on
+// dbase, u64 arrays) must sit on 8-byte boundaries for every shape in use.
+template <int V, int N>
+constexpr bool fold_smem_aligned() {
+    using S = FoldSmem<V, N>;
+    return offsetof(S, tk) % 8 == 0 && offsetof(S, tc) % 8 == 0 && offsetof(S, vs) % 8 == 0 &&
+           offsetof(S, svv) % 8 == 0 && offsetof(S, stag) % 8 == 0 && offsetof(S, dbase) % 8 == 0 &&
+           alignof(S) >= 8;
+}
+// (checked where each kernel instantiates its shape, fold_pipe_kernel)
+
 // Tuple tag: bits 15..8 = 0 for a document entry, (j+1)*2 for an entry of
 // source j, (j+1)*2+1 for its tombstone; bits 7..0 = tuple index in LDS.  The
 // sort order (key, tag) puts a key's tuples in replay order.
@@ -709,6 +720,8 @@ __global__ __launch_bounds__(fold_waves<DELTA>() * 64) __attribute__((amdgpu_wav
     static_assert(K >= 1 && K < 64, "a run's end bounds live in lane K: K < 64");
     constexpr int NCH = FoldShape<DELTA, LEAN>::NCH, VCH = FoldShape<DELTA, LEAN>::VCH;
     using Smem = FoldSmem<FoldShape<DELTA, LEAN>::VCAP, 64 * NCH>;
+    static_assert(fold_smem_aligned<FoldShape<DELTA, LEAN>::VCAP, 64 * NCH>(),
+                  "FoldSmem: a 64-bit LDS access target is not 8-byte aligned");
     __shared__ Smem smem[fold_waves<DELTA>()];
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t w = threadIdx.x >> 6;

@@ -28,7 +28,9 @@ __global__ __launch_bounds__(256) void check_order_kernel(const uint32_t* off, c
 __global__ __launch_bounds__(256) void pack_out_kernel(OutView in, const uint32_t* poff, uint32_t n, OutView out) {
     const uint32_t lane = threadIdx.x & 63;
     for (uint32_t d = uniform(blockIdx.x * 4 + (threadIdx.x >> 6)); d < n; d += gridDim.x * 4) {
-        const uint32_t o = in.offsets[d], p = poff[d], m = poff[d + 1] - p;
+        // a count above the document's own capacity (only after a failed merge)
+        // is clamped to it: the gather never leaves the document's region
+        const uint32_t o = in.offsets[d], p = poff[d], m = min(poff[d + 1] - p, in.offsets[d + 1] - o);
         for (uint32_t i = lane; i < m; i += 64) {
             out.keys[p + i] = in.keys[o + i];
             out.actors[p + i] = in.actors[o + i];

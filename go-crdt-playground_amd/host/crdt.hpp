@@ -611,8 +611,12 @@ inline bool aliased(const std::vector<AWSet*>& dsts, const std::vector<const AWS
 // Per document: plan (read only) then commit (the destination maps change).
 // Unaliased batches do both per document on its thread; aliased ones make
 // every plan first (strings copied), then commit.
+// The plan phase also takes the result's VersionVector width from the
+// pre-merge states: in an aliased batch another document's commit may be
+// rewriting a source's VV while this document commits.
 struct DocPlan {
-    Plan a, b;  // b: the second direction of an exchange
+    Plan a, b;      // b: the second direction of an exchange
+    size_t w = 0;   // len(dst.versionVector) after the merge
 };
 
 template <typename PlanFn, typename CommitFn>
@@ -928,11 +932,11 @@ inline void MergeBatch(const std::vector<AWSet*>& dsts, const std::vector<const 
             p.a.plan(b.dk, b.da, b.dc, b.dit, b.dfirst[d], b.dfirst[d + 1] - b.dfirst[d], co.keys, co.actors,
                      co.counters, co.offsets[d], co.counts[d], b.sk, b.sit, b.sfirst.data(), (uint32_t)d,
                      (uint32_t)d + 1);
+            p.w = std::max(b.dst[d]->versionVector.size(), b.src[d]->versionVector.size());
         },
-        [&](size_t d, DocPlan& p) {
-            const size_t w = std::max(b.dst[d]->versionVector.size(), b.src[d]->versionVector.size());
+        [&](size_t d, DocPlan& p) {  // writes only
             p.a.commit(*b.dst[d]);
-            set_vv(*b.dst[d], co.vv + d * b.R, w);
+            set_vv(*b.dst[d], co.vv + d * b.R, p.w);
         });
     LastStats().apply_s = secs_since(t0);
 }
@@ -972,13 +976,13 @@ inline void ExchangeBatch(const std::vector<AWSet*>& as, const std::vector<AWSet
             p.b.plan(b.sk, b.sa, b.sc, b.sit, b.sfirst[d], b.sfirst[d + 1] - b.sfirst[d], oba.keys, oba.actors,
                      oba.counters, oba.offsets[d], oba.counts[d], b.dk, b.dit, b.dfirst.data(), (uint32_t)d,
                      (uint32_t)d + 1);
+            p.w = std::max(as[d]->versionVector.size(), bs[d]->versionVector.size());
         },
         [&](size_t d, DocPlan& p) {  // ... then each map changes
-            const size_t w = std::max(as[d]->versionVector.size(), bs[d]->versionVector.size());
             p.a.commit(*as[d]);
             p.b.commit(*bs[d]);
-            set_vv(*as[d], oab.vv + d * b.R, w);
-            set_vv(*bs[d], oba.vv + d * b.R, w);
+            set_vv(*as[d], oab.vv + d * b.R, p.w);
+            set_vv(*bs[d], oba.vv + d * b.R, p.w);
         });
     LastStats().apply_s = secs_since(t0);
     LastStats().call_s = secs_since(t_call);
@@ -1049,12 +1053,12 @@ inline void fold(int mode, const std::vector<AWSet*>& dsts, const std::vector<st
             p.a.plan(b.dk, b.da, b.dc, b.dit, b.dfirst[d], b.dfirst[d + 1] - b.dfirst[d], co.keys, co.actors,
                      co.counters, co.offsets[d], co.counts[d], b.sk, b.sit, b.sfirst.data(), b.src_beg[d],
                      b.src_beg[d + 1]);
-        },
-        [&](size_t d, DocPlan& p) {
             const uint32_t s0 = b.src_beg[d], s1 = b.src_beg[d + 1];
-            const size_t w = fold_width(mode, *b.dst[d], b.src.data() + s0, s1 - s0);
+            p.w = fold_width(mode, *b.dst[d], b.src.data() + s0, s1 - s0);
+        },
+        [&](size_t d, DocPlan& p) {  // writes only
             p.a.commit(*b.dst[d]);
-            set_vv(*b.dst[d], co.vv + d * R, w);
+            set_vv(*b.dst[d], co.vv + d * R, p.w);
         });
     LastStats().apply_s = secs_since(t0);
 }

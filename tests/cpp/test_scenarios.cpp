@@ -236,6 +236,55 @@ static void TestBatches() {
     expect(d, {{"p", {1, 1}}, {"q", {2, 1}}}, {0, 2, 1});
 }
 
+// Aliased batches whose VersionVectors differ in length: every merge reads the
+// pre-batch snapshot, so each result's VV width is that of the snapshot's
+// states (crdt-misc.go:43-55 appends the longer tail), not of a source that
+// another document of the same batch has already merged into.
+static void TestAliasedRaggedWidths() {
+    for (int rep = 0; rep < 20; ++rep) {  // the commits run on several threads: repeat
+        std::vector<AWSet> s;
+        std::vector<AWSet> want;
+        for (int i = 0; i < 60; ++i) {  // chains a_i <- a_{i+1}, VV lengths 2,3,4,2,3,4,...
+            AWSet x((uint32_t)(i % 2), VersionVector(2 + i % 3, 0));
+            x.Add({"k" + std::to_string(i), "c"});
+            if (i % 4 == 1) x.Del({"c"});
+            s.push_back(x);
+        }
+        for (int i = 0; i + 1 < 60; ++i) {
+            AWSet x = s[i];
+            x.Merge(s[i + 1]);
+            want.push_back(x);
+        }
+        std::vector<AWSet*> d;
+        std::vector<const AWSet*> src;
+        for (int i = 0; i + 1 < 60; ++i) d.push_back(&s[i]), src.push_back(&s[i + 1]);
+        MergeBatch(d, src);
+        for (int i = 0; i + 1 < 60; ++i)
+            CHECK(s[i].entries == want[i].entries && s[i].versionVector == want[i].versionVector);
+    }
+    for (int rep = 0; rep < 20; ++rep) {
+        std::vector<AWSetDelta> s;
+        std::vector<AWSetDelta> want;
+        for (int i = 0; i < 60; ++i) {
+            AWSetDelta x((uint32_t)(i % 2), VersionVector(2 + i % 3, 0));
+            x.Add({"k" + std::to_string(i), "c"});
+            if (i % 4 == 1) x.Del({"c"});
+            s.push_back(x);
+        }
+        for (int i = 0; i + 1 < 60; ++i) {
+            AWSetDelta x = s[i];
+            x.Merge(s[i + 1]);
+            want.push_back(x);
+        }
+        std::vector<AWSetDelta*> d;
+        std::vector<std::vector<const AWSetDelta*>> src;
+        for (int i = 0; i + 1 < 60; ++i) d.push_back(&s[i]), src.push_back({&s[i + 1]});
+        DeltaMergeBatch(d, src);
+        for (int i = 0; i + 1 < 60; ++i)
+            CHECK(s[i].entries == want[i].entries && s[i].versionVector == want[i].versionVector);
+    }
+}
+
 // ExchangeBatch = the two merges of one snapshot, applied in place; an
 // aliased MergeBatch (a <- b and b <- a in one batch) reads the snapshot too.
 static void TestExchangeAndAliasing() {
@@ -275,6 +324,7 @@ static void TestExchangeAndAliasing() {
         threw = e.code == CRDT_E_INVALID;
     }
     CHECK(threw);  // a destination twice
+    TestAliasedRaggedWidths();
 }
 
 int main() {

@@ -827,3 +827,41 @@ def test_batch_key_order_checked_on_device(eng):
         with pytest.raises(crdtgpu.CrdtError) as ei:
             eng.fold(CRDT_FOLD_DELTA, fd, s2)
         assert ei.value.code == crdtgpu.CRDT_E_UNSORTED
+
+
+@pytest.mark.parametrize("what", ["tile_join", "tile_exchange", "block_fold_awset", "block_fold_delta"])
+def test_unsorted_large_documents_never_reach_the_merge(eng, what):
+    """An unsorted key in a tile-sized document (join / exchange: merge-path
+    tiles) or in a block-fold-sized document (> 256 tuples): the *_batch call
+    reads the device order check back before launching any merge kernel
+    (api.cpp order_gate) and returns CRDT_E_UNSORTED; the context stays usable."""
+    rng = random.Random(77)
+    R = 3
+    if what.startswith("tile"):
+        dst, src = join_case(rng, 40, R, lambda: rng.choice([3, 70, 3000]), 10 ** 6, 9)
+        d2, s2 = dst.numpy(), src.numpy()
+        big = max(range(40), key=lambda d: int(d2.offsets[d + 1] - d2.offsets[d]))
+        b = AWSetBatch(d2.R, d2.offsets.copy(), d2.keys.copy(), d2.actors, d2.counters, d2.vv, d2.counts)
+        o = int(b.offsets[big]) + 1500
+        b.keys[o], b.keys[o + 1] = b.keys[o + 1], b.keys[o]
+        with pytest.raises(crdtgpu.CrdtError) as ei:
+            eng.join(b, s2) if what == "tile_join" else eng.exchange(b, s2)
+        assert ei.value.code == crdtgpu.CRDT_E_UNSORTED
+        rc, want = oracle.join(d2, s2)  # the same context, sorted input: exact
+        assert rc == 0
+        assert_same(eng.join(d2, s2), want, d2.n_docs, R)
+        return
+    mode = CRDT_FOLD_AWSET if what.endswith("awset") else CRDT_FOLD_DELTA
+    fd, fs = fold_case(rng, 30, R, lambda: rng.choice([10, 400]), lambda: rng.randint(1, 4),
+                       lambda: rng.choice([5, 300]), lambda: rng.randint(0, 3), 5000, 9, mode == CRDT_FOLD_DELTA)
+    d2 = fd.numpy()
+    big = max(range(30), key=lambda d: int(d2.offsets[d + 1] - d2.offsets[d]))
+    b = AWSetBatch(d2.R, d2.offsets.copy(), d2.keys.copy(), d2.actors, d2.counters, d2.vv, d2.counts)
+    o = int(b.offsets[big]) + 200
+    b.keys[o], b.keys[o + 1] = b.keys[o + 1], b.keys[o]
+    with pytest.raises(crdtgpu.CrdtError) as ei:
+        eng.fold(mode, b, fs)
+    assert ei.value.code == crdtgpu.CRDT_E_UNSORTED
+    rc, want = oracle.fold(mode, fd, fs)
+    assert rc == 0
+    assert_same(eng.fold(mode, fd, fs), want, fd.n_docs, R)

@@ -1,0 +1,49 @@
+#!/bin/bash
+# The one GPU-box script: runs the named recipes in order, each GPU step under its
+# own time limit (tools/gpu_step.sh); a fault, abort or timeout ends the script.
+#
+#   bash tools/gpu_run.sh RECIPE...   (env: TAG=r04x, BENCH_ARGS="--config 3", CONFIGS="2 3 4 5")
+#
+# recipes:
+#   tests    pytest -m gpu (per-config parity tests first, tests/conftest.py)
+#   smoke    __graft_entry__.smoke()
+#   bench    default bench line -> gpurun_out/$TAG_bench.json
+#   prof     rocprofv3 kernel trace + stats of the bench (no CPU baseline) -> gpurun_out/prof_$TAG
+#   configs  bench + kernel trace per config in $CONFIGS
+#   pmc      PMC passes (tools/pmc.sh; one rocprofv3 --pmc run per counter group)
+#   probe    stamped fold probe (tools/fold_probe, built on the CPU side first)
+#   multi    the two-process device-summary test alone
+set -u
+cd "$(dirname "$0")/.."
+source tools/gpu_step.sh
+TAG=${TAG:-r04}
+BENCH_ARGS=${BENCH_ARGS:-}
+for r in "$@"; do
+  case $r in
+    tests)
+      TAILN=4 step gpu_tests 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread
+      grep -q " FAILED\| ERROR" gpurun_out/gpu_tests.log && { echo "tests failed"; exit 1; } ;;
+    smoke)
+      TAILN=2 step smoke 180 python -u -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench)
+      TAILN=1 step bench_$TAG 600 python3 bench.py $BENCH_ARGS
+      grep '^{"metric"' gpurun_out/bench_$TAG.log > gpurun_out/${TAG}_bench.json || true ;;
+    prof)
+      TAILN=2 step prof_$TAG 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$TAG -o run \
+        -- python3 bench.py --no-cpu-baseline $BENCH_ARGS ;;
+    configs)
+      for c in ${CONFIGS:-2 3 4 5}; do
+        TAILN=1 step bench_c${c}_$TAG 300 python3 bench.py --config $c $BENCH_ARGS
+        TAILN=3 step prof_c${c}_$TAG 300 rocprofv3 --kernel-trace --stats --output-format csv \
+          -d gpurun_out/prof_c${c}_$TAG -o run -- python3 bench.py --config $c --no-cpu-baseline $BENCH_ARGS
+      done ;;
+    pmc)
+      TAILN=10 step pmc_$TAG 1200 bash tools/pmc.sh ;;
+    probe)
+      TAILN=20 step probe_c3 120 tools/fold_probe 3
+      TAILN=20 step probe_c5 120 tools/fold_probe 5 ;;
+    multi)
+      TAILN=4 step multirank 300 python -u -m pytest tests/test_gpu_multirank.py -x -v --timeout 240 --timeout-method thread ;;
+    *) echo "unknown recipe $r"; exit 2 ;;
+  esac
+done
