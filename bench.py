@@ -8,7 +8,8 @@ state, R = 2, synthetic reachable states generated on the device
 document the two merges A <- B and B <- A of one snapshot (one exchange launch,
 crdt_awset_exchange_async), then the per-GPU causal-context summary
 (elementwise max of the output VVs), all-reduced (max, u64) across GPUs over
-RCCL when N > 1.
+RCCL when N > 1 -- on the engine's own communicator, through the C ABI
+(crdt_comm_init + crdt_context_allreduce_async), not torch's.
 
 The same JSON line carries one "legs" entry per other BASELINE config, each
 timed the same way (warmup, barrier + synchronize, K steps, max over ranks),
@@ -540,9 +541,10 @@ def run_config(config, n, args, ctx, steps, warmup, repeats, cpu, box=None):
         else:
             local_ctx = W.post(stream)
         if dist is not None:
-            if backend_is_host:
+            if backend_is_host:  # gloo rehearsal: torch.distributed on host copies
                 return u64_max_allreduce(dist, local_ctx.cpu()).to(dev)
-            return u64_max_allreduce(dist, local_ctx)
+            # the engine's own RCCL communicator, through the C ABI a Go caller binds
+            eng.context_allreduce_async(local_ctx, W.R, stream=stream)
         return local_ctx
 
     if graph is None:
@@ -743,6 +745,19 @@ def main():
     torch.cuda.set_device(dev)
     stream = torch.cuda.current_stream()
     eng = crdtgpu.Engine(gpu)
+    collective = None
+    if world > 1:
+        if backend == "nccl":
+            # crdt_comm_unique_id on rank 0, the id shared once over torch.distributed,
+            # crdt_comm_init on every rank: the per-step summary all-reduce is then
+            # crdt_context_allreduce_async (RCCL, u64 max) on the engine's communicator
+            from crdtgpu.dist import engine_comm_handshake
+
+            engine_comm_handshake(dist, world, rank, eng.comm_init)
+            collective = ("crdt_context_allreduce_async: RCCL all-reduce(max, u64) of R words on the engine's own "
+                          "communicator (crdt_comm_unique_id + crdt_comm_init), once per step")
+        else:
+            collective = "torch.distributed %s all-reduce of host copies (rehearsal)" % backend
     ctx = (eng, dev, stream, dist, world, rank)
 
     if args.legs is None:
@@ -770,6 +785,8 @@ def main():
         "data": "synthetic (AWSet states generated on device, csrc/gen.hip)",
     }
     result.update(head)
+    if collective:
+        result["config"]["collective"] = collective
     if box:
         result["box_probe"] = dict(box, what="crdt_bw_probe on this box before timing: streaming read (16 B/lane), "
                                              "write and copy (read+write bytes), best of nt/plain stores and 8/16/32 "

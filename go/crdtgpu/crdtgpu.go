@@ -1,0 +1,735 @@
+// Package crdtgpu is the MI355X merge path for package crdt
+// (rsms/go-crdt-playground), bound over cgo to libcrdtgpu.so (include/crdtgpu.h).
+//
+// UNTESTED HERE: the build image has no Go toolchain, so this file is neither
+// compiled nor run in this repository. It is the source a maintainer adds next
+// to the reference package. Every rule in it is exercised through the same C ABI
+// by the Python mirror (go-crdt-playground_amd/crdtgpu/awset.py,
+// tests/test_scenarios_gpu.py, tests/test_mirror_width.py) and the C++ mirror
+// (go-crdt-playground_amd/host/crdt.hpp, tests/cpp/test_scenarios.cpp).
+//
+// It keeps the reference types and adds batch entry points:
+//
+//	(*AWSet).Merge       awset.go:103-161           -> Engine.Merge / MergeBatch
+//	both directions      awset.go:103 twice          -> Engine.ExchangeBatch (one snapshot)
+//	ordered AWSet merges awset.go:103, in order      -> Engine.FoldBatch
+//	(*AWSetDelta).Merge  awset-delta_test.go:51-166  -> Engine.DeltaMerge / DeltaMergeBatch
+//
+// AWSetDelta lives in a _test.go file of the reference, invisible to importers,
+// so this package defines it (with Del and Clone, awset-delta_test.go:9-49).
+//
+// Needs Go >= 1.21 (min/max builtins, unsafe.SliceData).
+//
+// Host arrays come from crdt_host_alloc (page-locked C memory): the C structs
+// handed to the library then hold C pointers only, as cgo's pointer rules
+// require, and the uploads run at full PCIe rate.
+package crdtgpu
+
+/*
+#cgo CFLAGS: -I${SRCDIR}/../../include
+#cgo LDFLAGS: -L${SRCDIR}/../../go-crdt-playground_amd/crdtgpu -lcrdtgpu -Wl,-rpath,${SRCDIR}/../../go-crdt-playground_amd/crdtgpu
+#include "crdtgpu.h"
+*/
+import "C"
+
+import (
+	"fmt"
+	"sort"
+	"unsafe"
+
+	crdt "github.com/rsms/go-crdt-playground" // the reference package (no go.mod upstream: adjust the path)
+)
+
+// ---------------------------------------------------------------- engine
+
+// Engine is one library context (one per goroutine that issues calls).
+type Engine struct{ ctx *C.crdt_ctx }
+
+// NewEngine opens a context on a HIP device.
+func NewEngine(device int) (*Engine, error) {
+	var ctx *C.crdt_ctx
+	if rc := C.crdt_ctx_create(C.int(device), &ctx); rc != 0 {
+		return nil, errOf("crdt_ctx_create", rc)
+	}
+	return &Engine{ctx}, nil
+}
+
+// Close releases the context and its device workspaces.
+func (e *Engine) Close() {
+	if e.ctx != nil {
+		C.crdt_ctx_destroy(e.ctx)
+		e.ctx = nil
+	}
+}
+
+// Error is a library error; Code is a CRDT_E_* value. CRDT_E_ACTOR_RANGE is
+// where the reference panics (HasDot / Counter at actor == len(vv),
+// crdt-misc.go:29,37).
+type Error struct {
+	Call string
+	Code int
+}
+
+func (e *Error) Error() string {
+	return fmt.Sprintf("%s: %s", e.Call, C.GoString(C.crdt_strerror(C.int(e.Code))))
+}
+
+func errOf(call string, rc C.int) error { return &Error{call, int(rc)} }
+
+// ---------------------------------------------------------------- AWSetDelta
+
+// AWSetDelta is the reference's delta-state set (awset-delta_test.go:9-12).
+type AWSetDelta struct {
+	crdt.AWSet
+	Deleted map[string]crdt.Dot
+}
+
+// Del removes keys with one fresh dot for the whole call, recorded as a
+// tombstone for each key that was present (awset-delta_test.go:14-33).
+func (s *AWSetDelta) Del(keys ...string) {
+	s.VersionVector[s.Actor]++
+	dot := crdt.Dot{Actor: s.Actor, Counter: s.VersionVector[s.Actor]}
+	for _, k := range keys {
+		if _, ok := s.Entries[k]; !ok {
+			continue
+		}
+		if s.Deleted == nil {
+			s.Deleted = map[string]crdt.Dot{}
+		}
+		s.Deleted[k] = dot
+		delete(s.Entries, k)
+	}
+}
+
+// Clone is a deep copy (awset-delta_test.go:35-49).
+func (s *AWSetDelta) Clone() *AWSetDelta {
+	c := &AWSetDelta{AWSet: crdt.AWSet{Actor: s.Actor}}
+	c.VersionVector = append(crdt.VersionVector(nil), s.VersionVector...)
+	c.Entries = make(map[string]crdt.Dot, len(s.Entries))
+	for k, d := range s.Entries {
+		c.Entries[k] = d
+	}
+	if len(s.Deleted) > 0 {
+		c.Deleted = make(map[string]crdt.Dot, len(s.Deleted))
+		for k, d := range s.Deleted {
+			c.Deleted[k] = d
+		}
+	}
+	return c
+}
+
+// ---------------------------------------------------------------- page-locked arrays
+
+type arena struct {
+	blocks []unsafe.Pointer
+	err    error
+}
+
+func (a *arena) alloc(bytes int) unsafe.Pointer {
+	if bytes < 8 {
+		bytes = 8
+	}
+	var p unsafe.Pointer
+	if a.err == nil {
+		if rc := C.crdt_host_alloc(C.size_t(bytes), &p); rc != 0 {
+			a.err = errOf("crdt_host_alloc", rc)
+			return nil
+		}
+		a.blocks = append(a.blocks, p)
+	}
+	return p
+}
+
+func (a *arena) u64(n int) []uint64 {
+	p := a.alloc(n * 8)
+	if p == nil {
+		return make([]uint64, n) // never handed to C: a.err is set
+	}
+	return unsafe.Slice((*uint64)(p), n)
+}
+
+func (a *arena) u32(n int) []uint32 {
+	p := a.alloc(n * 4)
+	if p == nil {
+		return make([]uint32, n)
+	}
+	return unsafe.Slice((*uint32)(p), n)
+}
+
+func (a *arena) free() {
+	for _, p := range a.blocks {
+		C.crdt_host_free(p)
+	}
+	a.blocks = nil
+}
+
+func p64(s []uint64) *C.uint64_t { return (*C.uint64_t)(unsafe.Pointer(unsafe.SliceData(s))) }
+func p32(s []uint32) *C.uint32_t { return (*C.uint32_t)(unsafe.Pointer(unsafe.SliceData(s))) }
+
+// ---------------------------------------------------------------- interning
+
+// docKeys interns one document's keys: a key's id is its rank in string order
+// among every key of the document's states. The kernels compare keys of one
+// document only, so this is the exact order-preserving bijection they need,
+// built from one small sort per document (no batch-wide map).
+type docKeys []string
+
+func internDoc(maps ...map[string]crdt.Dot) docKeys {
+	seen := map[string]struct{}{}
+	var ks docKeys
+	for _, m := range maps {
+		for k := range m {
+			if _, ok := seen[k]; !ok {
+				seen[k] = struct{}{}
+				ks = append(ks, k)
+			}
+		}
+	}
+	sort.Strings(ks)
+	return ks
+}
+
+func (ks docKeys) id(k string) uint64 { return uint64(sort.SearchStrings(ks, k)) }
+
+// entries is a run of (key id, actor, counter) arrays in C memory.
+type entries struct {
+	keys     []uint64
+	actors   []uint32
+	counters []uint64
+}
+
+func (a *arena) entries(n int) entries { return entries{a.u64(n), a.u32(n), a.u64(n)} }
+
+// put writes m's entries, ascending by id, at e[at:]; returns the next position.
+func (e entries) put(at int, m map[string]crdt.Dot, ks docKeys) int {
+	ids := make([]uint64, 0, len(m))
+	for k := range m {
+		ids = append(ids, ks.id(k))
+	}
+	sort.Slice(ids, func(i, j int) bool { return ids[i] < ids[j] })
+	for _, id := range ids {
+		d := m[ks[id]]
+		e.keys[at], e.actors[at], e.counters[at] = id, uint32(d.Actor), uint64(d.Counter)
+		at++
+	}
+	return at
+}
+
+func putVV(dst []uint64, vv crdt.VersionVector) {
+	for i := range dst {
+		dst[i] = 0
+		if i < len(vv) {
+			dst[i] = uint64(vv[i])
+		}
+	}
+}
+
+// out is one merge output: document d's live entries are
+// [offsets[d], offsets[d] + counts[d]), its clock vv[d*R : d*R+R].
+type out struct {
+	offsets, counts []uint32
+	e               entries
+	vv              []uint64
+	c               C.crdt_awset_out
+}
+
+func (a *arena) out(n, R, slots int) *out {
+	o := &out{offsets: a.u32(n + 1), counts: a.u32(n), e: a.entries(slots + 1), vv: a.u64(n * R)}
+	o.c = C.crdt_awset_out{offsets: p32(o.offsets), counts: p32(o.counts), keys: p64(o.e.keys),
+		actors: p32(o.e.actors), counters: p64(o.e.counters), vv: p64(o.vv)}
+	return o
+}
+
+// apply writes document d of the output into dst (entries replaced, clock of
+// width w: VersionVector.Merge appends the longer tail, crdt-misc.go:43-55).
+func (o *out) apply(d, R, w int, ks docKeys, dst *crdt.AWSet) {
+	m := make(map[string]crdt.Dot, o.counts[d])
+	for j := o.offsets[d]; j < o.offsets[d]+o.counts[d]; j++ {
+		m[ks[o.e.keys[j]]] = crdt.Dot{Actor: crdt.Actor(o.e.actors[j]), Counter: uint(o.e.counters[j])}
+	}
+	dst.Entries = m
+	vv := make(crdt.VersionVector, w)
+	for r := 0; r < w; r++ {
+		vv[r] = uint(o.vv[d*R+r])
+	}
+	dst.VersionVector = vv
+}
+
+// batch packs one AWSet state per document.
+func (a *arena) batch(states []*crdt.AWSet, keys []docKeys, R int) (C.crdt_awset_batch, []uint32) {
+	n, total := len(states), 0
+	for _, s := range states {
+		total += len(s.Entries)
+	}
+	off, e, vv := a.u32(n+1), a.entries(total), a.u64(n*R)
+	at := 0
+	for d, s := range states {
+		off[d] = uint32(at)
+		if a.err == nil {
+			at = e.put(at, s.Entries, keys[d])
+			putVV(vv[d*R:(d+1)*R], s.VersionVector)
+		}
+	}
+	off[n] = uint32(total)
+	return C.crdt_awset_batch{n_docs: C.uint32_t(n), R: C.uint32_t(R), offsets: p32(off),
+		keys: p64(e.keys), actors: p32(e.actors), counters: p64(e.counters), vv: p64(vv)}, off
+}
+
+// ---------------------------------------------------------------- joins
+
+// Merge is dst.Merge(src) (awset.go:103) on the GPU: a one-document batch
+// (two PCIe round trips; batch many documents per call for throughput).
+func (e *Engine) Merge(dst, src *crdt.AWSet) error {
+	return e.MergeBatch([]*crdt.AWSet{dst}, []*crdt.AWSet{src})
+}
+
+// MergeBatch does dsts[i].Merge(srcs[i]) for every i in one call
+// (crdt_awset_join_batch). Destinations must be distinct. Every merge reads
+// the states as they were when the call began (a source that is also a
+// destination of the batch is read before it changes).
+func (e *Engine) MergeBatch(dsts, srcs []*crdt.AWSet) error {
+	if len(dsts) != len(srcs) {
+		return fmt.Errorf("MergeBatch: %d destinations, %d sources", len(dsts), len(srcs))
+	}
+	n := len(dsts)
+	if n == 0 {
+		return nil
+	}
+	if err := distinct(dsts); err != nil {
+		return err
+	}
+	docs := make([][]docState, n)
+	keys := make([]docKeys, n)
+	widths := make([]int, n)
+	for i := range dsts {
+		docs[i] = []docState{stateOf(dsts[i], nil), stateOf(srcs[i], nil)}
+		keys[i] = internDoc(dsts[i].Entries, srcs[i].Entries)
+		widths[i] = max(len(dsts[i].VersionVector), len(srcs[i].VersionVector))
+	}
+	R, err := raggedChecks(false, docs)
+	if err != nil {
+		return err
+	}
+	var a arena
+	defer a.free()
+	cd, doff := a.batch(dsts, keys, R)
+	cs, soff := a.batch(srcs, keys, R)
+	o := a.out(n, R, int(doff[n])+int(soff[n]))
+	if a.err != nil {
+		return a.err
+	}
+	if rc := C.crdt_awset_join_batch(e.ctx, &cd, &cs, &o.c); rc != 0 {
+		return errOf("crdt_awset_join_batch", rc)
+	}
+	for i, dst := range dsts {
+		o.apply(i, R, widths[i], keys[i], dst)
+	}
+	return nil
+}
+
+// ExchangeBatch is anti-entropy both ways in one call
+// (crdt_awset_exchange_batch): for every i, as[i] becomes
+// as[i].Clone().Merge(bs[i]) and bs[i] becomes bs[i].Clone().Merge(as[i]), the
+// two merges of ONE snapshot, from one read of the pair. This is not the
+// reference's sequential round trip a.Merge(b); b.Merge(a) (awset_test.go:15-16),
+// in which the second merge sees the updated a.
+func (e *Engine) ExchangeBatch(as, bs []*crdt.AWSet) error {
+	if len(as) != len(bs) {
+		return fmt.Errorf("ExchangeBatch: %d and %d states", len(as), len(bs))
+	}
+	n := len(as)
+	if n == 0 {
+		return nil
+	}
+	if err := distinct(append(append([]*crdt.AWSet(nil), as...), bs...)); err != nil {
+		return err
+	}
+	docs := make([][]docState, 0, 2*n)
+	keys := make([]docKeys, n)
+	widths := make([]int, n)
+	for i := range as {
+		docs = append(docs, []docState{stateOf(as[i], nil), stateOf(bs[i], nil)},
+			[]docState{stateOf(bs[i], nil), stateOf(as[i], nil)})
+		keys[i] = internDoc(as[i].Entries, bs[i].Entries)
+		widths[i] = max(len(as[i].VersionVector), len(bs[i].VersionVector))
+	}
+	R, err := raggedChecks(false, docs)
+	if err != nil {
+		return err
+	}
+	var a arena
+	defer a.free()
+	ca, aoff := a.batch(as, keys, R)
+	cb, boff := a.batch(bs, keys, R)
+	slots := int(aoff[n]) + int(boff[n])
+	oab, oba := a.out(n, R, slots), a.out(n, R, slots)
+	if a.err != nil {
+		return a.err
+	}
+	if rc := C.crdt_awset_exchange_batch(e.ctx, &ca, &cb, &oab.c, &oba.c); rc != 0 {
+		return errOf("crdt_awset_exchange_batch", rc)
+	}
+	for i := range as {
+		oab.apply(i, R, widths[i], keys[i], as[i])
+		oba.apply(i, R, widths[i], keys[i], bs[i])
+	}
+	return nil
+}
+
+// ---------------------------------------------------------------- ordered folds
+
+// FoldBatch does, for every i, dsts[i].Merge(s) for s in srcs[i] in order
+// (AWSet semantics, awset.go:103-161) in one call (crdt_awset_fold_batch).
+func (e *Engine) FoldBatch(dsts []*crdt.AWSet, srcs [][]*crdt.AWSet) error {
+	ds := make([]docState, len(dsts))
+	ss := make([][]docState, len(srcs))
+	for i, d := range dsts {
+		ds[i] = stateOf(d, nil)
+	}
+	for i, l := range srcs {
+		for _, s := range l {
+			ss[i] = append(ss[i], stateOf(s, nil))
+		}
+	}
+	return e.fold(false, dsts, ds, ss)
+}
+
+// DeltaMerge is dst.Merge(src) for AWSetDelta (awset-delta_test.go:51) on the GPU.
+func (e *Engine) DeltaMerge(dst, src *AWSetDelta) error {
+	return e.DeltaMergeBatch([]*AWSetDelta{dst}, [][]*AWSetDelta{{src}})
+}
+
+// DeltaMergeBatch does, for every i, dsts[i].Merge(s) for s in srcs[i] in
+// order (AWSetDelta semantics, awset-delta_test.go:51-166: the path select on
+// Counter(src.Actor), MakeDeltaMergeData's pruning, the no-op that skips even
+// the clock merge) in one call (crdt_awset_fold_batch, CRDT_FOLD_DELTA).
+// dsts[i].Deleted is not changed (the reference's merges never touch it).
+func (e *Engine) DeltaMergeBatch(dsts []*AWSetDelta, srcs [][]*AWSetDelta) error {
+	ad := make([]*crdt.AWSet, len(dsts))
+	ds := make([]docState, len(dsts))
+	ss := make([][]docState, len(srcs))
+	for i, d := range dsts {
+		ad[i] = &d.AWSet
+		ds[i] = stateOf(&d.AWSet, d.Deleted)
+	}
+	for i, l := range srcs {
+		for _, s := range l {
+			ss[i] = append(ss[i], stateOf(&s.AWSet, s.Deleted))
+		}
+	}
+	return e.fold(true, ad, ds, ss)
+}
+
+func (e *Engine) fold(delta bool, dsts []*crdt.AWSet, ds []docState, ss [][]docState) error {
+	if len(dsts) != len(ss) {
+		return fmt.Errorf("fold: %d destinations, %d source lists", len(dsts), len(ss))
+	}
+	n := len(dsts)
+	if n == 0 {
+		return nil
+	}
+	if err := distinct(dsts); err != nil {
+		return err
+	}
+	docs := make([][]docState, n)
+	keys := make([]docKeys, n)
+	widths := make([]int, n)
+	ns, nent, ntomb := 0, 0, 0
+	for i := range dsts {
+		docs[i] = append([]docState{ds[i]}, ss[i]...)
+		maps := []map[string]crdt.Dot{ds[i].Entries}
+		for _, s := range ss[i] {
+			maps = append(maps, s.Entries, s.Deleted)
+			nent += len(s.Entries)
+			ntomb += len(s.Deleted)
+		}
+		ns += len(ss[i])
+		keys[i] = internDoc(maps...)
+		widths[i] = foldWidth(delta, docs[i]) // from the snapshot, before any map changes
+	}
+	R, err := raggedChecks(delta, docs)
+	if err != nil {
+		return err
+	}
+	var a arena
+	defer a.free()
+	cd, doff := a.batch(dsts, keys, R)
+	docSrcs, srcActor, svv := a.u32(n+1), a.u32(ns), a.u64(ns*R)
+	eoff, ent := a.u32(ns+1), a.entries(nent)
+	var toff []uint32
+	var tomb entries
+	if delta && ntomb > 0 {
+		toff, tomb = a.u32(ns+1), a.entries(ntomb)
+	}
+	o := a.out(n, R, int(doff[n])+nent)
+	if a.err != nil {
+		return a.err
+	}
+	q, at, tat := 0, 0, 0
+	for i := range dsts {
+		docSrcs[i] = uint32(q)
+		for _, s := range ss[i] {
+			srcActor[q] = uint32(s.Actor)
+			putVV(svv[q*R:(q+1)*R], s.VersionVector)
+			eoff[q] = uint32(at)
+			at = ent.put(at, s.Entries, keys[i])
+			if toff != nil {
+				toff[q] = uint32(tat)
+				tat = tomb.put(tat, s.Deleted, keys[i])
+			}
+			q++
+		}
+	}
+	docSrcs[n], eoff[ns] = uint32(ns), uint32(nent)
+	cs := C.crdt_src_batch{n_docs: C.uint32_t(n), R: C.uint32_t(R), doc_srcs: p32(docSrcs),
+		src_actor: p32(srcActor), vv: p64(svv), entry_off: p32(eoff), keys: p64(ent.keys),
+		actors: p32(ent.actors), counters: p64(ent.counters)}
+	if toff != nil {
+		toff[ns] = uint32(ntomb)
+		cs.tomb_off, cs.tkeys, cs.tactors, cs.tcounters = p32(toff), p64(tomb.keys), p32(tomb.actors), p64(tomb.counters)
+	}
+	mode := C.int(C.CRDT_FOLD_AWSET)
+	if delta {
+		mode = C.CRDT_FOLD_DELTA
+	}
+	if rc := C.crdt_awset_fold_batch(e.ctx, mode, &cd, &cs, &o.c); rc != 0 {
+		return errOf("crdt_awset_fold_batch", rc)
+	}
+	for i, dst := range dsts {
+		o.apply(i, R, widths[i], keys[i], dst)
+	}
+	return nil
+}
+
+// foldWidth is len(dst.VersionVector) after the fold, replayed on the clocks
+// alone: every AWSet step merges the clock; a delta step merges it unless it
+// is the no-op (awset-delta_test.go:60): Counter(src.Actor) != 0 (:53) and
+// MakeDeltaMergeData finds no changed entry and no tombstone (:79-105). It
+// runs after raggedChecks would have refused a batch that panics in Go.
+func foldWidth(delta bool, doc []docState) int {
+	V := append(crdt.VersionVector(nil), doc[0].VersionVector...)
+	for _, s := range doc[1:] {
+		if delta && counterOf(V, s.Actor) != 0 {
+			brings := len(deletedOf(s)) > 0
+			for _, d := range s.Entries {
+				if !hasDotOf(V, d) {
+					brings = true
+					break
+				}
+			}
+			if !brings {
+				continue
+			}
+		}
+		V.Merge(s.VersionVector)
+	}
+	return len(V)
+}
+
+// deletedOf is MakeDeltaMergeData's deleted set (awset-delta_test.go:93-102):
+// tombstones whose key was not re-added with another or a newer dot.
+func deletedOf(s docState) map[string]crdt.Dot {
+	out := map[string]crdt.Dot{}
+	for k, x := range s.Deleted {
+		if m, ok := s.Entries[k]; ok && (m.Actor != x.Actor || m.Counter > x.Counter) {
+			continue
+		}
+		out[k] = x
+	}
+	return out
+}
+
+// panic-free HasDot / Counter for foldWidth (a panicking batch never gets here)
+func hasDotOf(vv crdt.VersionVector, d crdt.Dot) bool {
+	return int(d.Actor) < len(vv) && vv[d.Actor] >= d.Counter
+}
+
+func counterOf(vv crdt.VersionVector, a crdt.Actor) uint {
+	if int(a) < len(vv) {
+		return vv[a]
+	}
+	return 0
+}
+
+func distinct(states []*crdt.AWSet) error {
+	seen := make(map[*crdt.AWSet]struct{}, len(states))
+	for _, s := range states {
+		if _, ok := seen[s]; ok {
+			return fmt.Errorf("a state appears twice as a destination of one batch")
+		}
+		seen[s] = struct{}{}
+	}
+	return nil
+}
+
+// ---------------------------------------------------------------- ragged clocks
+
+// docState is one state of a document: the destination, or one of its
+// ordered sources (Deleted: AWSetDelta.Deleted, nil for an AWSet).
+type docState struct {
+	Actor         crdt.Actor
+	VersionVector crdt.VersionVector
+	Entries       map[string]crdt.Dot
+	Deleted       map[string]crdt.Dot
+}
+
+func stateOf(s *crdt.AWSet, deleted map[string]crdt.Dot) docState {
+	return docState{s.Actor, s.VersionVector, s.Entries, deleted}
+}
+
+type goPanic struct{}
+
+// checks evaluates HasDot / Counter as Go does on the unpadded vectors
+// (crdt-misc.go:28-41) and notes where the zero-padded width R answers
+// differently (a counter-0 dot at len(vv) < actor < R).
+type checks struct {
+	R          int
+	padDiffers bool
+}
+
+func (c *checks) has(vv crdt.VersionVector, d crdt.Dot) bool {
+	if len(vv) < int(d.Actor) {
+		if int(d.Actor) < c.R && d.Counter == 0 {
+			c.padDiffers = true
+		}
+		return false
+	}
+	if int(d.Actor) == len(vv) {
+		panic(goPanic{})
+	}
+	return vv[d.Actor] >= d.Counter
+}
+
+func (c *checks) counter(vv crdt.VersionVector, a crdt.Actor) uint {
+	if len(vv) < int(a) {
+		return 0
+	}
+	if int(a) == len(vv) {
+		panic(goPanic{})
+	}
+	return vv[a]
+}
+
+// replayChecks replays doc[0].Merge(doc[j]) for j = 1.. in order on copies of
+// the maps, with the reference's rules (awset.go:107-161; for delta,
+// awset-delta_test.go:51-166), only to learn whether Go panics (1) or the
+// padded layout would differ (2). The merged entries come from the GPU.
+func replayChecks(delta bool, doc []docState, R int) (res int) {
+	c := checks{R: R}
+	defer func() {
+		if r := recover(); r != nil {
+			if _, ok := r.(goPanic); !ok {
+				panic(r)
+			}
+			res = 1
+		}
+	}()
+	V := append(crdt.VersionVector(nil), doc[0].VersionVector...)
+	E := make(map[string]crdt.Dot, len(doc[0].Entries))
+	for k, d := range doc[0].Entries {
+		E[k] = d
+	}
+	for _, s := range doc[1:] {
+		full := !delta || c.counter(V, s.Actor) == 0 // awset-delta_test.go:53
+		changed, deleted := s.Entries, map[string]crdt.Dot(nil)
+		if !full { // MakeDeltaMergeData, awset-delta_test.go:79-105
+			changed = map[string]crdt.Dot{}
+			for k, d := range s.Entries {
+				if !c.has(V, d) {
+					changed[k] = d
+				}
+			}
+			deleted = deletedOf(s)
+			if len(changed) == 0 && len(deleted) == 0 {
+				continue // :60 -- not even the VV merge
+			}
+		}
+		for k, sd := range changed { // phase 1: awset.go:122-143, awset-delta_test.go:126-147
+			if _, ok := E[k]; ok || !c.has(V, sd) {
+				E[k] = sd
+			}
+		}
+		if full { // phase 2: awset.go:145-159
+			for k, d := range E {
+				if _, ok := s.Entries[k]; !ok && c.has(s.VersionVector, d) {
+					delete(E, k)
+				}
+			}
+		} else { // phase 2: awset-delta_test.go:149-164
+			for k, x := range deleted {
+				if _, ok := E[k]; ok && !c.has(V, x) {
+					delete(E, k)
+				}
+			}
+		}
+		V.Merge(s.VersionVector)
+	}
+	if c.padDiffers {
+		return 2
+	}
+	return 0
+}
+
+// raggedChecks picks the batch's padded width R (>= every vector's length,
+// clear of the actors of documents with a shorter vector: the kernels flag
+// actor == R) and replays those documents. Equal-length documents need no
+// host work: the kernels flag actor == R exactly where Go panics.
+func raggedChecks(delta bool, docs [][]docState) (int, error) {
+	R := 1
+	for _, doc := range docs {
+		for _, s := range doc {
+			R = max(R, len(s.VersionVector))
+		}
+	}
+	short := func(doc []docState, w int) bool {
+		for _, s := range doc {
+			if len(s.VersionVector) < w {
+				return true
+			}
+		}
+		return false
+	}
+	hasActor := func(doc []docState, w int) bool {
+		for j, s := range doc {
+			if j > 0 && delta && int(s.Actor) == w {
+				return true
+			}
+			for _, m := range []map[string]crdt.Dot{s.Entries, s.Deleted} {
+				for _, d := range m {
+					if int(d.Actor) == w {
+						return true
+					}
+				}
+			}
+		}
+		return false
+	}
+	w := R
+	for ; w <= C.CRDT_MAX_R; w++ {
+		clash := false
+		for _, doc := range docs {
+			if short(doc, w) && hasActor(doc, w) {
+				clash = true
+				break
+			}
+		}
+		if !clash {
+			break
+		}
+	}
+	if w > C.CRDT_MAX_R {
+		return 0, fmt.Errorf("no padded width <= %d clear of the actors", C.CRDT_MAX_R)
+	}
+	for _, doc := range docs {
+		if !short(doc, w) {
+			continue
+		}
+		switch replayChecks(delta, doc, w) {
+		case 1:
+			return 0, &Error{"raggedChecks", int(C.CRDT_E_ACTOR_RANGE)} // Go panics here
+		case 2:
+			return 0, fmt.Errorf("counter-0 dot beyond a shorter version vector (not representable padded)")
+		}
+	}
+	return w, nil
+}

@@ -3,6 +3,7 @@ declares, and its host-only entry points (validation, strerror) behave.  No
 compute call is made here (no GPU in this container)."""
 
 import ctypes
+import os
 
 import numpy as np
 import pytest
@@ -115,3 +116,21 @@ def test_engine_needs_a_gpu_or_works():
 def test_single_hip_runtime_in_process():
     """torch and libcrdtgpu.so must share one HIP runtime (torch streams are passed in)."""
     assert len(abi.hip_runtimes_mapped()) <= 1, abi.hip_runtimes_mapped()
+
+
+def test_go_binding_calls_declared_entry_points():
+    """go/crdtgpu/crdtgpu.go (not compiled here: no Go toolchain) calls only C
+    names that include/crdtgpu.h declares, and binds the batch entry points."""
+    import re
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    go = open(os.path.join(root, "go", "crdtgpu", "crdtgpu.go")).read()
+    hdr = open(os.path.join(root, "include", "crdtgpu.h")).read()
+    used = set(re.findall(r"\bC\.(crdt_\w+|CRDT_\w+)", go))
+    assert used
+    for name in used:
+        assert re.search(r"\b%s\b" % name, hdr), name
+    for must in ("crdt_awset_join_batch", "crdt_awset_exchange_batch", "crdt_awset_fold_batch", "crdt_host_alloc"):
+        assert must in used
+    code = re.sub(r'//[^\n]*|"(?:[^"\\]|\\.)*"', "", go)  # comments and string literals out
+    assert code.count("{") == code.count("}") and code.count("(") == code.count(")")

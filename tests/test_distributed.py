@@ -65,6 +65,42 @@ def test_global_context_allreduce_gloo(world):
         assert g == want
 
 
+def _handshake_worker(rank, world, port, q):
+    import torch.distributed as dist
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    seen = []
+    uid = cdist.engine_comm_handshake(dist, world, rank, lambda w, r, u: seen.append((w, r, u)))
+    q.put((rank, uid, seen))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_engine_comm_id_handshake_gloo(world):
+    """bench.py's multi-rank setup of the engine's own RCCL communicator,
+    rehearsed over gloo: rank 0's crdt_comm_unique_id (RCCL loads on a host
+    without a GPU) reaches every rank unchanged, and every rank calls
+    crdt_comm_init's stand-in exactly once with (world, its rank, that id)."""
+    import torch.multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_handshake_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in ps)
+    for p in ps:
+        p.join(60)
+        assert p.exitcode == 0
+    uid = res[0][1]
+    assert len(uid) == 128 and any(uid)
+    for rank, u, seen in res:
+        assert u == uid and seen == [(world, rank, uid)]
+
+
 def test_shard_covers_all_docs():
     for n, w in [(0, 2), (1, 2), (10, 3), (100_000_000, 8), (7, 8)]:
         spans = [cdist.shard(n, w, r) for r in range(w)]
