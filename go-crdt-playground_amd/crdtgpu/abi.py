@@ -40,6 +40,8 @@ CRDT_PROBE_WRITE = 1
 CRDT_PROBE_COPY = 2
 CRDT_PROBE_WRITE_PLAIN = 3
 CRDT_PROBE_COPY_PLAIN = 4
+CRDT_PROBE_MIX = 5
+CRDT_PROBE_MIX_PLAIN = 6
 
 _vp = ctypes.c_void_p
 _u32 = ctypes.c_uint32

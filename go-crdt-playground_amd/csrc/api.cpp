@@ -622,7 +622,7 @@ int crdt_gen_zipf_async(crdt_ctx* ctx, uint64_t seed, uint32_t n_docs, const uin
 }
 
 int crdt_bw_probe(crdt_ctx* ctx, int kind, const void* a, void* b, size_t bytes, int reps, double* gbs) {
-    if (!ctx || !gbs || kind < CRDT_PROBE_READ || kind > CRDT_PROBE_COPY_PLAIN || reps < 1 || bytes < 16 || !b ||
+    if (!ctx || !gbs || kind < CRDT_PROBE_READ || kind > CRDT_PROBE_MIX_PLAIN || reps < 1 || bytes < 16 || !b ||
         (kind != CRDT_PROBE_WRITE && kind != CRDT_PROBE_WRITE_PLAIN && !a))
         return CRDT_E_INVALID;
     int rc = set_device(ctx);
@@ -647,7 +647,9 @@ int crdt_bw_probe(crdt_ctx* ctx, int kind, const void* a, void* b, size_t bytes,
     if (e0) (void)hipEventDestroy(e0);
     if (e1) (void)hipEventDestroy(e1);
     if (rc == CRDT_OK) {
-        const double moved = (double)n16 * 16.0 * ((kind == CRDT_PROBE_COPY || kind == CRDT_PROBE_COPY_PLAIN) ? 2.0 : 1.0);
+        const bool mix = kind == CRDT_PROBE_MIX || kind == CRDT_PROBE_MIX_PLAIN;
+        const double moved = mix ? (double)(n16 / 4) * 16.0 * 7.0
+                                 : (double)n16 * 16.0 * ((kind == CRDT_PROBE_COPY || kind == CRDT_PROBE_COPY_PLAIN) ? 2.0 : 1.0);
         *gbs = ms > 0.f ? moved * reps / (ms * 1e-3) / 1e9 : 0.0;
     }
     return leave(ctx, s, cap, rc);

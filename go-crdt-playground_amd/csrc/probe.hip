@@ -5,7 +5,10 @@
 //
 //   read : 16 B per lane loads, four in flight per lane, grid-stride
 //   write: 16 B per lane non-temporal stores (the merge kernels' output stores)
-//   copy : both, one read and one write per 16 B (the merges' mixed shape)
+//   copy : both, one read and one write per 16 B
+//   mix  : 3 reads : 4 writes of 16 B (the config-2 exchange's measured mix,
+//          2.85 GB read : 3.72 GB written per launch -- it writes more than
+//          it reads, so the 1:1 copy is not its ceiling)
 #include "crdt_device.hpp"
 
 namespace crdt {
@@ -57,6 +60,20 @@ __global__ __launch_bounds__(256) void probe_copy_kernel(const u32x4* __restrict
     for (; i < n; i += stride) put16<NT>(a[i], b + i);
 }
 
+// q = a quarter of the buffer in 16-byte words: reads a[i], a[i+q], a[i+2q],
+// writes b[i], b[i+q], b[i+2q], b[i+3q] -- 7 x 16 B moved per i, 3:4.
+template <bool NT>
+__global__ __launch_bounds__(256) void probe_mix_kernel(const u32x4* __restrict__ a, u32x4* __restrict__ b, size_t q) {
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < q; i += stride) {
+        const u32x4 x0 = a[i], x1 = a[i + q], x2 = a[i + 2 * q];
+        put16<NT>(x0, b + i);
+        put16<NT>(x1, b + i + q);
+        put16<NT>(x2, b + i + 2 * q);
+        put16<NT>(x0 ^ x1 ^ x2, b + i + 3 * q);
+    }
+}
+
 // Shader clock under load: every CU runs dependent VALU chains; wave 0 of
 // block 0 reads the shader-cycle counter (s_memtime) and the fixed-rate
 // wall clock (s_memrealtime) around its loop.  out[0] = cycles, out[1] =
@@ -86,7 +103,8 @@ hipError_t launch_clock_probe(uint64_t* out, uint32_t n_cu, hipStream_t stream) 
 }
 
 // kind (crdtgpu.h CRDT_PROBE_*): 0 read a, 1 write b (nt), 2 copy a -> b (nt),
-// 3 write b (plain stores), 4 copy (plain stores); n16 = 16-byte words;
+// 3 write b (plain stores), 4 copy (plain stores), 5 mix 3 reads : 4 writes
+// (nt), 6 mix (plain stores); n16 = 16-byte words;
 // blocks_per_cu workgroups of 256 threads per CU.
 hipError_t launch_probe(int kind, const void* a, void* b, size_t n16, uint32_t n_cu, uint32_t blocks_per_cu,
                         hipStream_t stream) {
@@ -98,6 +116,8 @@ hipError_t launch_probe(int kind, const void* a, void* b, size_t n16, uint32_t n
         case 1: hipLaunchKernelGGL(probe_write_kernel<true>, dim3(grid), dim3(256), 0, stream, dst, n16); break;
         case 2: hipLaunchKernelGGL(probe_copy_kernel<true>, dim3(grid), dim3(256), 0, stream, src, dst, n16); break;
         case 3: hipLaunchKernelGGL(probe_write_kernel<false>, dim3(grid), dim3(256), 0, stream, dst, n16); break;
+        case 5: hipLaunchKernelGGL(probe_mix_kernel<true>, dim3(grid), dim3(256), 0, stream, src, dst, n16 / 4); break;
+        case 6: hipLaunchKernelGGL(probe_mix_kernel<false>, dim3(grid), dim3(256), 0, stream, src, dst, n16 / 4); break;
         default: hipLaunchKernelGGL(probe_copy_kernel<false>, dim3(grid), dim3(256), 0, stream, src, dst, n16); break;
     }
     return hipGetLastError();

@@ -231,6 +231,8 @@ int crdt_gen_replicas_async(crdt_ctx* ctx, uint64_t seed, uint32_t n_docs, uint3
 #define CRDT_PROBE_COPY 2
 #define CRDT_PROBE_WRITE_PLAIN 3
 #define CRDT_PROBE_COPY_PLAIN 4
+#define CRDT_PROBE_MIX 5       /* 3 reads : 4 writes of 16 B (the exchange's mix), nt stores; GB/s = all 7 */
+#define CRDT_PROBE_MIX_PLAIN 6 /* the same, plain stores */
 int crdt_bw_probe(crdt_ctx* ctx, int kind, const void* a, void* b, size_t bytes, int reps, double* gbs);
 /* The shader clock (MHz) while every CU runs dependent integer chains:
  * shader-cycle counter over the fixed-rate wall clock on one wave.  Kernels
