@@ -118,9 +118,12 @@ class AWSetBatch:
 
 
 class OutBuffers:
-    """Output of a join/fold: n_docs docs, `slots` capacity, numpy or torch."""
+    """Output of a join/fold: n_docs docs, `slots` capacity, numpy or torch.
+    shared_keys: another OutBuffers whose key column this one uses (the two
+    outputs of an exchange hold the same keys at the same slots,
+    crdt_awset_exchange_async)."""
 
-    def __init__(self, n_docs, R, slots, device=None):
+    def __init__(self, n_docs, R, slots, device=None, shared_keys=None):
         self.R, self.n_docs, self.slots = int(R), int(n_docs), int(slots)
         if device is None:
             self.offsets = np.zeros(n_docs + 1, dtype=U32)
@@ -135,10 +138,13 @@ class OutBuffers:
             e = lambda n, dt: torch.empty(max(n, 1), dtype=dt, device=device)  # noqa: E731
             self.offsets = e(n_docs + 1, torch.int32)[: n_docs + 1]
             self.counts = e(n_docs, torch.int32)[:n_docs]
-            self.keys = e(slots, torch.int64)
+            self.keys = e(slots if shared_keys is None else 0, torch.int64)
             self.actors = e(slots, torch.int32)
             self.counters = e(slots, torch.int64)
             self.vv = e(n_docs * R, torch.int64)
+        if shared_keys is not None:
+            assert shared_keys.slots >= self.slots
+            self.keys = shared_keys.keys
 
     def c(self) -> CAWSetOut:
         return CAWSetOut(ptr(self.offsets), ptr(self.counts), ptr(self.keys), ptr(self.actors), ptr(self.counters),

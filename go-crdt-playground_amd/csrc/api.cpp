@@ -16,7 +16,8 @@
 
 namespace crdt {
 hipError_t launch_join(const BatchView& dst, const BatchView& src, const OutView& out, const OutView* out2,
-                       const Work& wk, uint32_t docs_per_wave, bool nt_stores, uint32_t block_grid, bool no_large,
+                       const Work& wk, uint32_t docs_per_wave, bool nt_stores, bool stage_stores, uint32_t block_grid,
+                       bool no_large,
                        const TileWork* tw, uint32_t n_cu, hipStream_t stream);
 hipError_t launch_fold(int mode, const BatchView& dst, const SrcView& sb, const OutView& out, const Scratch& scr,
                        const Work& wk, uint32_t block_grid, bool lean_first, hipStream_t stream);
@@ -125,6 +126,7 @@ struct crdt_ctx {
     uint32_t max_doc_entries = 0xFFFFFFFFu;  // caller's promise (crdt_ctx_set_max_doc_entries)
     uint32_t join_docs_per_wave = 8;          // crdt_ctx_set_option("join_docs_per_wave")
     bool join_nt_stores = true;               // crdt_ctx_set_option("join_nt_stores")
+    bool join_stage_stores = true;            // crdt_ctx_set_option("join_stage_stores")
     bool fold_lean_first = true;              // crdt_ctx_set_option("fold_lean_first")
     uint32_t probe_blocks_per_cu = 16;        // crdt_ctx_set_option("probe_blocks_per_cu")
     bool pack_outputs = false;                // crdt_ctx_set_option("pack_batch_outputs")
@@ -376,6 +378,10 @@ int crdt_ctx_set_option(crdt_ctx* ctx, const char* name, int64_t value) {
         ctx->join_nt_stores = value != 0;
         return CRDT_OK;
     }
+    if (!strcmp(name, "join_stage_stores")) {
+        ctx->join_stage_stores = value != 0;
+        return CRDT_OK;
+    }
     return CRDT_E_INVALID;
 }
 
@@ -435,7 +441,7 @@ static int join_common(crdt_ctx* ctx, const crdt_awset_batch* dst, const crdt_aw
     OutView o2v;
     if (out2) o2v = view(out2);
     rc = hip_err(launch_join(view(dst), view(src), view(out), out2 ? &o2v : nullptr, make_work(ctx),
-                             ctx->join_docs_per_wave, ctx->join_nt_stores, block_grid(ctx), no_large,
+                             ctx->join_docs_per_wave, ctx->join_nt_stores, ctx->join_stage_stores, block_grid(ctx), no_large,
                              tiles ? &tw : nullptr, (uint32_t)ctx->n_cu, s));
     return leave(ctx, s, cap, rc);
 }
@@ -447,7 +453,11 @@ int crdt_awset_join_async(crdt_ctx* ctx, const crdt_awset_batch* dst, const crdt
 
 int crdt_awset_exchange_async(crdt_ctx* ctx, const crdt_awset_batch* a, const crdt_awset_batch* b,
                               const crdt_awset_out* out_ab, const crdt_awset_out* out_ba, void* stream) {
-    if (!out_ab || !out_ba || out_ab->keys == out_ba->keys) return CRDT_E_INVALID;
+    // out_ba->keys == out_ab->keys: one shared key column (both directions hold
+    // the same keys at the same slots); every other array must be its own
+    if (!out_ab || !out_ba || out_ab->actors == out_ba->actors || out_ab->counters == out_ba->counters ||
+        out_ab->vv == out_ba->vv || out_ab->counts == out_ba->counts)
+        return CRDT_E_INVALID;
     return join_common(ctx, a, b, out_ab, out_ba, stream);
 }
 

@@ -81,12 +81,14 @@ __device__ __forceinline__ void lanes_issue(JoinLanes& L, const BatchView& dst, 
     L.vs = ld64(make_rsrc(src.vv + vo, rv * 8u), o8);
 }
 
+// Per wave: key[0..64) dst keys, key[64..128) src keys; vv[0..64) dst VV,
+// vv[64..128) src VV.  Staged stores (STG) then reuse key/vv/act as the
+// document's output image: keys, counters and actors by output slot.
 template <int WAVES>
 struct JoinWaveSmem {
-    uint64_t dkey[WAVES][64];
-    uint64_t skey[WAVES][64];
-    uint64_t dvv[WAVES][64];
-    uint64_t svv[WAVES][64];
+    uint64_t key[WAVES][128];
+    uint64_t vv[WAVES][128];
+    uint32_t act[WAVES][128];
 };
 
 // Merge document d whose entries are in L (awset.go:107-161).  AUX: cache
@@ -95,8 +97,13 @@ struct JoinWaveSmem {
 // directions keep the same keys at the same slots (a dst-only key survives iff
 // srcVV has not seen it, a src-only key iff dstVV has not, in either
 // direction); only a common key's dot differs -- the src dot wins
-// (awset.go:142), so out2 takes the dst lane's own dot.
-template <int WAVES, int AUX, bool EXCH>
+// (awset.go:142), so out2 takes the dst lane's own dot.  out2.keys may be
+// out.keys (one shared key column): its key stores are then skipped.
+// STG: survivors are placed in LDS by output slot first and each output array
+// is written lane l -> slot l (and l + 64): every store instruction covers
+// whole contiguous cache lines, instead of the dst lanes and the src lanes
+// each writing an interleaved subset of the same lines.
+template <int WAVES, int AUX, bool EXCH, bool STG>
 __device__ __forceinline__ void join_doc(JoinWaveSmem<WAVES>& sm, uint32_t w, const JoinLanes& L, const JoinMeta& m,
                                          uint32_t d, bool small, const OutView& out, const OutView& out2,
                                          uint32_t n_docs, uint32_t end_off, uint32_t R, uint32_t lane, uint64_t lt,
@@ -104,20 +111,24 @@ __device__ __forceinline__ void join_doc(JoinWaveSmem<WAVES>& sm, uint32_t w, co
     const uint32_t obase = m.doff + m.soff;
     const uint32_t dnn = small ? m.dn : 0u, snn = small ? m.sn : 0u;
     const bool dv = lane < dnn, sv = lane < snn;
-    sm.dvv[w][lane] = L.vd;
-    sm.svv[w][lane] = L.vs;
-    sm.dkey[w][lane] = L.dk;
-    sm.skey[w][lane] = L.sk;
+    uint64_t* const dkey = sm.key[w];
+    uint64_t* const skey = sm.key[w] + 64;
+    uint64_t* const dvv = sm.vv[w];
+    uint64_t* const svv = sm.vv[w] + 64;
+    dvv[lane] = L.vd;
+    svv[lane] = L.vs;
+    dkey[lane] = L.dk;
+    skey[lane] = L.sk;
     wave_sync();
     // # src keys < dk, # dst keys < sk
-    const uint32_t j = lower_bound_pow<6>(sm.skey[w], snn, L.dk);
-    const uint32_t i = lower_bound_pow<6>(sm.dkey[w], dnn, L.sk);
-    const bool dmatch = dv && j < snn && sm.skey[w][j & 63] == L.dk;
-    const bool smatch = sv && i < dnn && sm.dkey[w][i & 63] == L.sk;
+    const uint32_t j = lower_bound_pow<6>(skey, snn, L.dk);
+    const uint32_t i = lower_bound_pow<6>(dkey, dnn, L.sk);
+    const bool dmatch = dv && j < snn && skey[j & 63] == L.dk;
+    const bool smatch = sv && i < dnn && dkey[i & 63] == L.sk;
     // awset.go:145-159: a dst-only key survives unless src's clock covers it.
-    const bool dh = has_dot_bf(sm.svv[w], R, L.da, L.dc, dv && !dmatch, err);
+    const bool dh = has_dot_bf(svv, R, L.da, L.dc, dv && !dmatch, err);
     // awset.go:130-140: a src-only key is added unless dst's clock covers it.
-    const bool sh = has_dot_bf(sm.dvv[w], R, L.sa, L.sc, sv && !smatch, err);
+    const bool sh = has_dot_bf(dvv, R, L.sa, L.sc, sv && !smatch, err);
     const bool dkeep = dv && (dmatch || !dh);
     const bool skeep = sv && !smatch && !sh;
     const uint64_t dm = ballot(dkeep), smk = ballot(skeep);
@@ -126,36 +137,94 @@ __device__ __forceinline__ void join_doc(JoinWaveSmem<WAVES>& sm, uint32_t w, co
     const uint64_t mc = __shfl(L.sc, (int)(j & 63));
     const uint32_t dpos = below(dm) + popc(smk & low_mask(j));
     const uint32_t spos = below(smk) + popc(dm & low_mask(i));
-    const uint32_t cap = dnn + snn;
-    const rsrc_t ok = make_rsrc(out.keys + obase, cap * 8u);
-    const rsrc_t oa = make_rsrc(out.actors + obase, cap * 4u);
-    const rsrc_t oc = make_rsrc(out.counters + obase, cap * 8u);
-    const uint32_t d8 = dkeep ? dpos * 8u : kOOB, d4 = dkeep ? dpos * 4u : kOOB;
-    const uint32_t s8 = skeep ? spos * 8u : kOOB, s4 = skeep ? spos * 4u : kOOB;
-    st64<AUX>(L.dk, ok, d8);
-    st32<AUX>(dmatch ? ma : L.da, oa, d4);
-    st64<AUX>(dmatch ? mc : L.dc, oc, d8);
-    st64<AUX>(L.sk, ok, s8);
-    st32<AUX>(L.sa, oa, s4);
-    st64<AUX>(L.sc, oc, s8);
+    const uint32_t n_out = popc(dm) + popc(smk);
+    const bool kshare = EXCH && out2.keys == out.keys;
+    if (STG) {
+        // the output image: slot -> key / counter / actor (out = dst <- src)
+        uint64_t* const ik = sm.key[w];
+        uint64_t* const ic = sm.vv[w];
+        uint32_t* const ia = sm.act[w];
+        wave_sync();  // every lane's probes of this document are done
+        if (dkeep) {
+            ik[dpos] = L.dk;
+            ic[dpos] = dmatch ? mc : L.dc;
+            ia[dpos] = dmatch ? ma : L.da;
+        }
+        if (skeep) {
+            ik[spos] = L.sk;
+            ic[spos] = L.sc;
+            ia[spos] = L.sa;
+        }
+        wave_sync();
+        const uint64_t k0 = ik[lane], k1 = ik[lane + 64], c0 = ic[lane], c1 = ic[lane + 64];
+        const uint32_t a0 = ia[lane], a1 = ia[lane + 64];
+        const rsrc_t ok = make_rsrc(out.keys + obase, n_out * 8u);
+        const rsrc_t oa = make_rsrc(out.actors + obase, n_out * 4u);
+        const rsrc_t oc = make_rsrc(out.counters + obase, n_out * 8u);
+        st64<AUX>(k0, ok, lane * 8u);
+        st64<AUX>(k1, ok, lane * 8u + 512u);
+        st32<AUX>(a0, oa, lane * 4u);
+        st32<AUX>(a1, oa, lane * 4u + 256u);
+        st64<AUX>(c0, oc, lane * 8u);
+        st64<AUX>(c1, oc, lane * 8u + 512u);
+        if (EXCH) {
+            // out2 = src <- dst: the same image but a common key keeps the dst dot
+            wave_sync();
+            if (dmatch) {
+                ic[dpos] = L.dc;
+                ia[dpos] = L.da;
+            }
+            wave_sync();
+            const uint64_t e0 = ic[lane], e1 = ic[lane + 64];
+            const uint32_t b0 = ia[lane], b1 = ia[lane + 64];
+            const rsrc_t pk = make_rsrc(out2.keys + obase, kshare ? 0u : n_out * 8u);
+            const rsrc_t pa = make_rsrc(out2.actors + obase, n_out * 4u);
+            const rsrc_t pc = make_rsrc(out2.counters + obase, n_out * 8u);
+            if (!kshare) {
+                st64<AUX>(k0, pk, lane * 8u);
+                st64<AUX>(k1, pk, lane * 8u + 512u);
+            }
+            st32<AUX>(b0, pa, lane * 4u);
+            st32<AUX>(b1, pa, lane * 4u + 256u);
+            st64<AUX>(e0, pc, lane * 8u);
+            st64<AUX>(e1, pc, lane * 8u + 512u);
+        }
+    } else {
+        const uint32_t cap = dnn + snn;
+        const rsrc_t ok = make_rsrc(out.keys + obase, cap * 8u);
+        const rsrc_t oa = make_rsrc(out.actors + obase, cap * 4u);
+        const rsrc_t oc = make_rsrc(out.counters + obase, cap * 8u);
+        const uint32_t d8 = dkeep ? dpos * 8u : kOOB, d4 = dkeep ? dpos * 4u : kOOB;
+        const uint32_t s8 = skeep ? spos * 8u : kOOB, s4 = skeep ? spos * 4u : kOOB;
+        st64<AUX>(L.dk, ok, d8);
+        st32<AUX>(dmatch ? ma : L.da, oa, d4);
+        st64<AUX>(dmatch ? mc : L.dc, oc, d8);
+        st64<AUX>(L.sk, ok, s8);
+        st32<AUX>(L.sa, oa, s4);
+        st64<AUX>(L.sc, oc, s8);
+        if (EXCH) {
+            const rsrc_t pk = make_rsrc(out2.keys + obase, kshare ? 0u : cap * 8u);
+            const rsrc_t pa = make_rsrc(out2.actors + obase, cap * 4u);
+            const rsrc_t pc = make_rsrc(out2.counters + obase, cap * 8u);
+            if (!kshare) {
+                st64<AUX>(L.dk, pk, d8);
+                st64<AUX>(L.sk, pk, s8);
+            }
+            st32<AUX>(L.da, pa, d4);
+            st64<AUX>(L.dc, pc, d8);
+            st32<AUX>(L.sa, pa, s4);
+            st64<AUX>(L.sc, pc, s8);
+        }
+    }
     // slot bounds (every doc), live count and VV (wave path only)
     const bool last = d == n_docs - 1;
     const uint64_t vmax = L.vd > L.vs ? L.vd : L.vs;  // awset.go:160 -> crdt-misc.go:43-55
     st32(lane == 0 ? obase : end_off, make_rsrc(out.offsets + d, last ? 8u : 4u), lane < 2 ? lane * 4u : kOOB);
-    st32(popc(dm) + popc(smk), make_rsrc(out.counts + d, small ? 4u : 0u), lane == 0 ? 0u : kOOB);
+    st32(n_out, make_rsrc(out.counts + d, small ? 4u : 0u), lane == 0 ? 0u : kOOB);
     st64(vmax, make_rsrc(out.vv + (size_t)d * R, small ? R * 8u : 0u), lane * 8u);
     if (EXCH) {
-        const rsrc_t pk = make_rsrc(out2.keys + obase, cap * 8u);
-        const rsrc_t pa = make_rsrc(out2.actors + obase, cap * 4u);
-        const rsrc_t pc = make_rsrc(out2.counters + obase, cap * 8u);
-        st64<AUX>(L.dk, pk, d8);
-        st32<AUX>(L.da, pa, d4);
-        st64<AUX>(L.dc, pc, d8);
-        st64<AUX>(L.sk, pk, s8);
-        st32<AUX>(L.sa, pa, s4);
-        st64<AUX>(L.sc, pc, s8);
         st32(lane == 0 ? obase : end_off, make_rsrc(out2.offsets + d, last ? 8u : 4u), lane < 2 ? lane * 4u : kOOB);
-        st32(popc(dm) + popc(smk), make_rsrc(out2.counts + d, small ? 4u : 0u), lane == 0 ? 0u : kOOB);
+        st32(n_out, make_rsrc(out2.counts + d, small ? 4u : 0u), lane == 0 ? 0u : kOOB);
         st64(vmax, make_rsrc(out2.vv + (size_t)d * R, small ? R * 8u : 0u), lane * 8u);
     }
     wave_sync();
@@ -168,7 +237,7 @@ __device__ __forceinline__ void join_doc(JoinWaveSmem<WAVES>& sm, uint32_t w, co
 // ping-pong pipeline -- the next document's entries are issued before this
 // one is merged.  The body is straight-line buffer VMEM, so the compiler's
 // vmcnt waits count exactly and the prefetch stays in flight.
-template <int WAVES, int K, int AUX, bool EXCH>
+template <int WAVES, int K, int AUX, bool EXCH, bool STG>
 __global__ __launch_bounds__(WAVES * 64) void join_wave_kernel(BatchView dst, BatchView src, OutView out, OutView out2,
                                                                Work wk, uint32_t no_large) {
     __shared__ JoinWaveSmem<WAVES> sm;
@@ -207,7 +276,7 @@ __global__ __launch_bounds__(WAVES * 64) void join_wave_kernel(BatchView dst, Ba
         uint32_t dn = d + WAVES;
         bool small_n = more && mn.dn <= 64 && mn.sn <= 64;
         lanes_issue(LB, dst, src, mn, dn, small_n, lane, R);
-        join_doc<WAVES, AUX, EXCH>(sm, w, LA, m, d, small, out, out2, n_docs, end_off, R, lane, lt, err);
+        join_doc<WAVES, AUX, EXCH, STG>(sm, w, LA, m, d, small, out, out2, n_docs, end_off, R, lane, lt, err);
         if (!small) push_large(d);
         if (!more) break;
         ++k;
@@ -220,7 +289,7 @@ __global__ __launch_bounds__(WAVES * 64) void join_wave_kernel(BatchView dst, Ba
         dn = d + WAVES;
         small_n = more && mn.dn <= 64 && mn.sn <= 64;
         lanes_issue(LA, dst, src, mn, dn, small_n, lane, R);
-        join_doc<WAVES, AUX, EXCH>(sm, w, LB, m, d, small, out, out2, n_docs, end_off, R, lane, lt, err);
+        join_doc<WAVES, AUX, EXCH, STG>(sm, w, LB, m, d, small, out, out2, n_docs, end_off, R, lane, lt, err);
         if (!small) push_large(d);
         if (!more) break;
         ++k;
@@ -278,29 +347,39 @@ constexpr int kJoinWaves = 4;
 constexpr int kBlockNT = 256;
 constexpr int kBlockIPT = 4;
 
-template <int K, int AUX, bool EXCH>
+template <int K, int AUX, bool EXCH, bool STG>
 static void launch_wave(const BatchView& dst, const BatchView& src, const OutView& out, const OutView& out2,
                         const Work& wk, bool no_large, hipStream_t stream) {
     const uint32_t per_block = kJoinWaves * K;
     const uint32_t grid = (dst.n_docs + per_block - 1) / per_block;
-    hipLaunchKernelGGL((join_wave_kernel<kJoinWaves, K, AUX, EXCH>), dim3(grid), dim3(kJoinWaves * 64), 0, stream,
+    hipLaunchKernelGGL((join_wave_kernel<kJoinWaves, K, AUX, EXCH, STG>), dim3(grid), dim3(kJoinWaves * 64), 0, stream,
                        dst, src, out, out2, wk, (uint32_t)no_large);
 }
 
-template <int AUX, bool EXCH>
+template <int AUX, bool EXCH, bool STG>
 static void launch_wave_k(uint32_t k, const BatchView& dst, const BatchView& src, const OutView& out,
                           const OutView& out2, const Work& wk, bool no_large, hipStream_t stream) {
     switch (k) {
-        case 1: launch_wave<1, AUX, EXCH>(dst, src, out, out2, wk, no_large, stream); break;
-        case 2: launch_wave<2, AUX, EXCH>(dst, src, out, out2, wk, no_large, stream); break;
-        case 4: launch_wave<4, AUX, EXCH>(dst, src, out, out2, wk, no_large, stream); break;
-        case 16: launch_wave<16, AUX, EXCH>(dst, src, out, out2, wk, no_large, stream); break;
-        default: launch_wave<8, AUX, EXCH>(dst, src, out, out2, wk, no_large, stream); break;
+        case 1: launch_wave<1, AUX, EXCH, STG>(dst, src, out, out2, wk, no_large, stream); break;
+        case 2: launch_wave<2, AUX, EXCH, STG>(dst, src, out, out2, wk, no_large, stream); break;
+        case 4: launch_wave<4, AUX, EXCH, STG>(dst, src, out, out2, wk, no_large, stream); break;
+        case 16: launch_wave<16, AUX, EXCH, STG>(dst, src, out, out2, wk, no_large, stream); break;
+        default: launch_wave<8, AUX, EXCH, STG>(dst, src, out, out2, wk, no_large, stream); break;
     }
 }
 
+template <bool EXCH, bool STG>
+static void launch_wave_ks(uint32_t k, bool nt_stores, const BatchView& dst, const BatchView& src, const OutView& out,
+                           const OutView& out2, const Work& wk, bool no_large, hipStream_t stream) {
+    if (nt_stores)
+        launch_wave_k<kAuxNT, EXCH, STG>(k, dst, src, out, out2, wk, no_large, stream);
+    else
+        launch_wave_k<0, EXCH, STG>(k, dst, src, out, out2, wk, no_large, stream);
+}
+
 // docs_per_wave: K of join_wave_kernel (1, 2, 4, 8 or 16); nt_stores: write the
-// output with non-temporal stores; no_large: the caller promised every doc has
+// output with non-temporal stores; stage_stores: place the survivors in LDS by
+// output slot and write whole contiguous lines (join_doc's STG); no_large: the caller promised every doc has
 // <= 64 entries per side, so the block path is not launched (a larger doc then
 // raises CRDT_E_INVALID).  out2 != nullptr: exchange -- also out2 = src <- dst.
 hipError_t launch_join_tiles(const BatchView& A, const BatchView& B, const OutView& o1, const OutView* o2,
@@ -310,20 +389,20 @@ hipError_t launch_join_tiles(const BatchView& A, const BatchView& B, const OutVi
 // (tile.hip); the per-document block kernel then only runs when the tiles
 // exceed the workspace (tw->fallback).
 hipError_t launch_join(const BatchView& dst, const BatchView& src, const OutView& out, const OutView* out2,
-                       const Work& wk, uint32_t docs_per_wave, bool nt_stores, uint32_t block_grid, bool no_large,
-                       const TileWork* tw, uint32_t n_cu, hipStream_t stream) {
+                       const Work& wk, uint32_t docs_per_wave, bool nt_stores, bool stage_stores, uint32_t block_grid,
+                       bool no_large, const TileWork* tw, uint32_t n_cu, hipStream_t stream) {
     if (dst.n_docs == 0) return hipSuccess;
     const OutView& o2 = out2 ? *out2 : out;
     if (out2) {
-        if (nt_stores)
-            launch_wave_k<kAuxNT, true>(docs_per_wave, dst, src, out, o2, wk, no_large, stream);
+        if (stage_stores)
+            launch_wave_ks<true, true>(docs_per_wave, nt_stores, dst, src, out, o2, wk, no_large, stream);
         else
-            launch_wave_k<0, true>(docs_per_wave, dst, src, out, o2, wk, no_large, stream);
+            launch_wave_ks<true, false>(docs_per_wave, nt_stores, dst, src, out, o2, wk, no_large, stream);
     } else {
-        if (nt_stores)
-            launch_wave_k<kAuxNT, false>(docs_per_wave, dst, src, out, o2, wk, no_large, stream);
+        if (stage_stores)
+            launch_wave_ks<false, true>(docs_per_wave, nt_stores, dst, src, out, o2, wk, no_large, stream);
         else
-            launch_wave_k<0, false>(docs_per_wave, dst, src, out, o2, wk, no_large, stream);
+            launch_wave_ks<false, false>(docs_per_wave, nt_stores, dst, src, out, o2, wk, no_large, stream);
     }
     hipError_t e = hipGetLastError();
     if (e != hipSuccess || no_large) return e;

@@ -657,18 +657,24 @@ def test_exchange_equals_two_joins(eng, torch, sizes):
     assert_same(o2, w2, a.n_docs, R)
 
 
-def test_exchange_config2_full_size(eng, torch):
+@pytest.mark.parametrize("stage,shared", [(1, 0), (1, 1), (0, 0), (0, 1)])
+def test_exchange_config2_full_size(eng, torch, stage, shared):
+    """All 1,048,576 config-2 docs, both directions, vs the oracle joins: LDS-
+    staged contiguous stores (the default) and the lane-scattered stores, each
+    with its own and with one shared key column (out_ba.keys = out_ab.keys)."""
     n = 1 << 20
     A, B = gen_pair(eng, torch, n, 0x5EED)
     dev = torch.device("cuda:0")
     oab = OutBuffers(n, 2, 2 * n * 64, device=dev)
-    oba = OutBuffers(n, 2, 2 * n * 64, device=dev)
+    oba = OutBuffers(n, 2, 2 * n * 64, device=dev, shared_keys=oab if shared else None)
     eng.set_max_doc_entries(64)
+    eng.set_option("join_stage_stores", stage)
     try:
         eng.exchange_async(A.as_batch(), B.as_batch(), oab, oba)
         eng.sync()
     finally:
         eng.set_max_doc_entries()
+        eng.set_option("join_stage_stores", 1)
     ha, hb = host_out(A, torch).as_batch(), host_out(B, torch).as_batch()
     rc, want = oracle.join(ha, hb)
     assert rc == 0
@@ -676,6 +682,32 @@ def test_exchange_config2_full_size(eng, torch):
     rc, want = oracle.join(hb, ha)
     assert rc == 0
     assert_same_all(host_out(oba, torch), want, n, 2)
+
+
+@pytest.mark.parametrize("stage", [1, 0])
+def test_exchange_shared_key_column_mixed_sizes(eng, torch, stage):
+    """One shared key column for both exchange outputs on the wave, tile and
+    block paths (documents of 0 ... 2000 entries per side), device buffers."""
+    rng = random.Random(43)
+    R = 3
+    a, b = join_case(rng, 300, R, lambda: rng.choice([0, 5, 63, 64, 65, 300, 2000]), 5000, 9)
+    dev = torch.device("cuda:0")
+    da, db = a.to(dev), b.to(dev)
+    slots = int(a.offsets[-1]) + int(b.offsets[-1])
+    o1 = OutBuffers(a.n_docs, R, slots, device=dev)
+    o2 = OutBuffers(a.n_docs, R, slots, device=dev, shared_keys=o1)
+    eng.set_option("join_stage_stores", stage)
+    try:
+        eng.exchange_async(da, db, o1, o2)
+        eng.sync()
+    finally:
+        eng.set_option("join_stage_stores", 1)
+    rc, w1 = oracle.join(a, b)
+    assert rc == 0
+    rc, w2 = oracle.join(b, a)
+    assert rc == 0
+    assert_same(host_out(o1, torch), w1, a.n_docs, R)
+    assert_same(host_out(o2, torch), w2, a.n_docs, R)
 
 
 def test_max_doc_entries_promise_is_checked(eng):

@@ -13,6 +13,8 @@
 #   pmc      PMC passes (tools/pmc.sh; one rocprofv3 --pmc run per counter group)
 #   probe    stamped fold probe (tools/fold_probe, built on the CPU side first)
 #   multi    the two-process device-summary test alone
+#   xab      config-2 exchange store forms A/B (tools/exchange_ab.py)
+#   ptest    pytest -m gpu on $PTEST (a -k expression)
 set -u
 cd "$(dirname "$0")/.."
 source tools/gpu_step.sh
@@ -44,6 +46,11 @@ for r in "$@"; do
       TAILN=20 step probe_c5 120 tools/fold_probe 5 ;;
     multi)
       TAILN=4 step multirank 300 python -u -m pytest tests/test_gpu_multirank.py -x -v --timeout 240 --timeout-method thread ;;
+    xab)
+      TAILN=12 step xab_$TAG 300 python3 tools/exchange_ab.py ;;
+    ptest)
+      TAILN=6 step ptest_$TAG 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -k "$PTEST"
+      grep -q " FAILED\| ERROR" gpurun_out/ptest_$TAG.log && { echo "tests failed"; exit 1; } ;;
     *) echo "unknown recipe $r"; exit 2 ;;
   esac
 done
