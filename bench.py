@@ -159,6 +159,7 @@ class Config2:
     kernel = "join_wave_kernel"
     metric = "replica-merges/sec (AWSet full-state join) + achieved HBM GB/s (% roofline)"
     exchange = True  # both merges from one read (crdt_awset_exchange_async); --separate: two join launches
+    shared_keys = True  # the two outputs share one key column (same keys, same slots); --own-keys: one each
     cpu_docs = 65536
 
     def __init__(self, eng, n, seed, dev, stream):
@@ -174,11 +175,15 @@ class Config2:
         self.B = OutBuffers(n, R, n * 64, device=dev)
         eng.gen_pair_async(seed, n, self.A, self.B, stream=stream)
         self.oab = OutBuffers(n, R, 2 * n * 64, device=dev)
-        self.oba = OutBuffers(n, R, 2 * n * 64, device=dev)
+        self.oba = OutBuffers(n, R, 2 * n * 64, device=dev, shared_keys=self._key_owner())
         self.ctx_ab = torch.zeros(R, dtype=torch.int64, device=dev)
         self.ctx_ba = torch.zeros(R, dtype=torch.int64, device=dev)
         self.a, self.b = self.A.as_batch(), self.B.as_batch()
         self.merges_per_step = 2 * n
+
+    def _key_owner(self):
+        """B <- A uses A <- B's key column when the exchange shares one."""
+        return self.oab if (self.exchange and self.shared_keys) else None
 
     def _structs(self):
         if not hasattr(self, "_cs"):
@@ -218,17 +223,23 @@ class Config2:
         cab, cba = self.oab.counts.cpu().numpy(), self.oba.counts.cpu().numpy()
         per_merge = workloads.join_bytes(cA, cB, cab, self.R) + workloads.join_bytes(cB, cA, cba, self.R)
         if self.exchange:
-            return workloads.exchange_bytes(cA, cB, cab, cba, self.R), per_merge
+            return workloads.exchange_bytes(cA, cB, cab, cba, self.R, self.exchange and self.shared_keys), per_merge
         return per_merge // 2, per_merge
 
     @property
     def kernel_name(self):
-        return self.kernel + (" (exchange: both merges of one snapshot, one read)" if self.exchange else "")
+        return self.kernel + ((" (exchange: both merges of one snapshot, one read; %s)" % self._keys_what())
+                              if self.exchange else "")
+
+    def _keys_what(self):
+        return ("one key column shared by the two outputs, survivors staged in LDS and stored as whole lines"
+                if self.shared_keys else "a key column per output, survivors staged in LDS and stored as whole lines")
 
     def describe(self, world):
         return {"workload": "config2: %d docs/GPU x 2 replicas x 64 entries, R=2, full-state join: the two merges "
                             "A<-B and B<-A of one snapshot (%s) + causal-context allreduce(max,u64)" % (
-                                self.n, "one exchange launch" if self.exchange else "two join launches"),
+                                self.n, ("one exchange launch, " + self._keys_what()) if self.exchange
+                                else "two join launches"),
                 "docs_per_gpu": self.n, "replicas": 2, "entries_per_replica": 64, "R": self.R,
                 "merges_per_step": self.merges_per_step * world, "parallelism": "doc-sharded x%d" % world}
 
@@ -254,6 +265,9 @@ class Config4(Config2):
     R = 2
     name = "config4"
     kernel = "join_tile_pipe_kernel"
+    # the tile kernel is latency-bound: one shared key column saves 0.3 % of its
+    # time (9.84 vs 9.87 ms), so this leg keeps a key column per output
+    shared_keys = False
     metric = "replica-merges/sec (AWSet join, Zipf sizes, config 4) + achieved HBM GB/s (% roofline)"
     cpu_docs = 96
 
@@ -277,7 +291,7 @@ class Config4(Config2):
         self.B = OutBuffers(n, R, self.total, device=dev)
         eng.gen_zipf_async(seed, n, self.d_offs, self.A, self.B, stream=stream)
         self.oab = OutBuffers(n, R, 2 * self.total, device=dev)
-        self.oba = OutBuffers(n, R, 2 * self.total, device=dev)
+        self.oba = OutBuffers(n, R, 2 * self.total, device=dev, shared_keys=self._key_owner())
         self.ctx_ab = torch.zeros(R, dtype=torch.int64, device=dev)
         self.ctx_ba = torch.zeros(R, dtype=torch.int64, device=dev)
         self.a, self.b = self.A.as_batch(), self.B.as_batch()
@@ -288,7 +302,8 @@ class Config4(Config2):
     def kernel_name(self):
         return ("join_tile_pipe_kernel (exchange call: join_wave_kernel for docs <= 64 per side, tile plan, merge-path "
                 "tiles of 1024 positions placed by a look-back deferred by one tile, stores in aligned 64-slot windows; "
-                "timed as the whole call)")
+                "%s; timed as the whole call)" % ("one key column shared by the two outputs" if self.shared_keys
+                                                  else "a key column per output"))
 
     def describe(self, world):
         return {"workload": "config4: %d docs/GPU, Zipf(1.1)-like sizes in [1, 2^20) (mean %.0f, max %d, %d entries "
@@ -460,8 +475,10 @@ def _traffic(path, config, n, W):
         return None
     try:
         for e in json.load(open(path)):
+            exch = bool(getattr(W, "exchange", False))
             if (e.get("docs") == n and e.get("config") == config and e.get("kernel", "").startswith(W.kernel)
-                    and bool(e.get("exchange")) == bool(getattr(W, "exchange", False))):
+                    and bool(e.get("exchange")) == exch
+                    and (not exch or bool(e.get("shared_keys", False)) == bool(W.shared_keys))):
                 return e.get("hbm_bytes_per_launch")
     except Exception:
         return None
@@ -494,6 +511,8 @@ def run_config(config, n, args, ctx, steps, warmup, repeats, cpu, box=None):
     cls = CONFIGS[config]
     if args.separate and config in (2, 4):
         cls.exchange = False
+    if args.own_keys and config in (2, 4):
+        cls.shared_keys = False
     W = cls(eng, n, seed, dev, stream)
     eng.sync(stream)
 
@@ -712,6 +731,8 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=3.0, help="seconds per CPU baseline variant")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--separate", action="store_true", help="configs 2/4: two join launches instead of one exchange")
+    ap.add_argument("--own-keys", action="store_true",
+                    help="configs 2/4: a key column per exchange output instead of one shared column")
     ap.add_argument("--no-graph", action="store_true", help="launch eagerly instead of replaying a captured HIP graph")
     ap.add_argument("--no-boundary", action="store_true", help="skip the host boundary-cost leg")
     ap.add_argument("--no-box-probe", action="store_true", help="skip the box bandwidth probes")

@@ -194,12 +194,15 @@ def join_bytes(n_dst, n_src, n_out, R) -> int:
     return int(20 * (n_dst.sum() + n_src.sum() + n_out.sum()) + (24 * R + 12) * n_dst.size)
 
 
-def exchange_bytes(n_a, n_b, n_ab, n_ba, R) -> int:
+def exchange_bytes(n_a, n_b, n_ab, n_ba, R, shared_keys=False) -> int:
     """One exchange launch (A <- B and B <- A from one read of both states):
     Σ over docs of 20(n_a + n_b) read once + 20(n_ab + n_ba) written +
-    32R (two VVs read, two written) + 32 (offsets and counts: two read, two written)."""
+    32R (two VVs read, two written) + 32 (offsets and counts: two read, two written).
+    shared_keys: the two outputs share one key column (n_ab == n_ba, the same
+    keys at the same slots), so B <- A writes 12 B per entry (actor, counter)."""
     n_a, n_b, n_ab, n_ba = (np.asarray(x, dtype=np.int64) for x in (n_a, n_b, n_ab, n_ba))
-    return int(20 * (n_a.sum() + n_b.sum() + n_ab.sum() + n_ba.sum()) + (32 * R + 32) * n_a.size)
+    out_b = 12 if shared_keys else 20
+    return int(20 * (n_a.sum() + n_b.sum() + n_ab.sum()) + out_b * n_ba.sum() + (32 * R + 32) * n_a.size)
 
 
 def fold_bytes(n_dst, n_out, src_entries, src_tombs, n_srcs_total, R) -> int:

@@ -689,6 +689,17 @@ struct DocMeta {
     uint32_t d, doff, slots, n, s0, ms, e0, E, t0, X, N, big;
 };
 
+// 1: survivors staged through LDS and written as contiguous lines -- measured
+// 4 % slower on config 3 and 5 % on config 5 (tools/fold_probe.hip timing
+// builds, three interleaved rounds), so off: each lane stores its own
+// survivors at their slots.  (CRDT_FOLD_NO_STORES, a diagnostic bound that
+// writes nothing, is only 4 % faster: the folds are not bound by their stores.)
+#ifndef CRDT_FOLD_STAGE_STORES
+#define CRDT_FOLD_STAGE_STORES 0
+#endif
+#ifndef CRDT_FOLD_NO_STORES
+#define CRDT_FOLD_NO_STORES 0
+#endif
 #ifndef CRDT_FOLD_WAVES
 #define CRDT_FOLD_WAVES 2
 #endif
@@ -1173,6 +1184,41 @@ __global__ __launch_bounds__(fold_waves<DELTA>() * 64) __attribute__((amdgpu_wav
             for (int q = 0; q < NCH; ++q) em.off[q] = kOOB;
             U = 0;
         }
+#if CRDT_FOLD_NO_STORES  // diagnostic bound (tools/fold_probe): the survivors are not written
+#pragma unroll
+        for (int q = 0; q < NCH; ++q) {
+            st64<kFoldStoreAux>(em.k[q], ok, kOOB);
+            st32<kFoldStoreAux>(em.a[q], oa, kOOB);
+            st64<kFoldStoreAux>(em.c[q], oc, kOOB);
+        }
+#elif CRDT_FOLD_STAGE_STORES
+        // The survivors are placed by output slot in LDS (tk / ta / tc are dead
+        // once the resolve is done), then each array is written lane l -> slot
+        // c * 64 + l: every store instruction covers contiguous whole lines.
+        wave_sync();
+#pragma unroll
+        for (int q = 0; q < NCH; ++q) {
+            const uint32_t o = em.off[q];
+            if (o != kOOB) {
+                m.tk[o] = em.k[q];
+                m.ta[o] = em.a[q];
+                m.tc[o] = em.c[q];
+            }
+        }
+        wave_sync();
+        {
+            const rsrc_t sk = make_rsrc(out.keys + obase, min(U, capo) * 8u);
+            const rsrc_t sa = make_rsrc(out.actors + obase, min(U, capo) * 4u);
+            const rsrc_t sc = make_rsrc(out.counters + obase, min(U, capo) * 8u);
+#pragma unroll
+            for (int q = 0; q < NCH; ++q) {
+                const uint32_t i = q * 64u + lane;
+                st64<kFoldStoreAux>(m.tk[i], sk, i * 8u);
+                st32<kFoldStoreAux>(m.ta[i], sa, i * 4u);
+                st64<kFoldStoreAux>(m.tc[i], sc, i * 8u);
+            }
+        }
+#else
 #pragma unroll
         for (int q = 0; q < NCH; ++q) {
             const uint32_t o = em.off[q];
@@ -1181,6 +1227,7 @@ __global__ __launch_bounds__(fold_waves<DELTA>() * 64) __attribute__((amdgpu_wav
             st32<kFoldStoreAux>(em.a[q], oa, o4);
             st64<kFoldStoreAux>(em.c[q], oc, o8);
         }
+#endif
         const uint32_t carry = U;
         const bool none = cur.big || deferred;
         st32(carry, make_rsrc(out.counts + cur.d, none ? 0u : 4u), lane == 0 ? 0u : kOOB);

@@ -422,7 +422,9 @@ __device__ __forceinline__ void tile_stores(const TileSmem<NT, IPT>& sm, const T
     const uint32_t d = uniform(cur.d);
     const rsrc_t k1 = make_rsrc_u(o1.keys + obase, nb * 8u), a1 = make_rsrc_u(o1.actors + obase, nb * 4u),
                  c1 = make_rsrc_u(o1.counters + obase, nb * 8u);
-    const rsrc_t k2 = make_rsrc_u(o2.keys + obase, EXCH ? nb * 8u : 0u),
+    // o2.keys == o1.keys: one shared key column, written once (the store
+    // still issues, out of range, so the count of memory operations is fixed)
+    const rsrc_t k2 = make_rsrc_u(o2.keys + obase, (EXCH && o2.keys != o1.keys) ? nb * 8u : 0u),
                  a2 = make_rsrc_u(o2.actors + obase, EXCH ? nb * 4u : 0u),
                  c2 = make_rsrc_u(o2.counters + obase, EXCH ? nb * 8u : 0u);
     const uint32_t shift = ALIGN ? (uint32_t)(obase & 63u) : 0u;

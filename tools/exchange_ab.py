@@ -40,7 +40,7 @@ def run(form, reps):
         eng.exchange_async(a, b, o1, o2s if form[1] else o2, stream=s)
     e1.record(s)
     e1.synchronize()
-    return e0.elapsed_time(e1) / reps
+    return e0.elapsed_time(e1) / max(reps, 1)
 
 
 def snapshot(form):

@@ -15,6 +15,7 @@
 #   multi    the two-process device-summary test alone
 #   xab      config-2 exchange store forms A/B (tools/exchange_ab.py)
 #   ptest    pytest -m gpu on $PTEST (a -k expression)
+#   ftime    fold timing builds tools/fold_time_$FTIME (space-separated variant names), interleaved, configs 3 and 5
 set -u
 cd "$(dirname "$0")/.."
 source tools/gpu_step.sh
@@ -46,6 +47,10 @@ for r in "$@"; do
       TAILN=20 step probe_c5 120 tools/fold_probe 5 ;;
     multi)
       TAILN=4 step multirank 300 python -u -m pytest tests/test_gpu_multirank.py -x -v --timeout 240 --timeout-method thread ;;
+    ftime)
+      for r in 1 2 3; do for v in ${FTIME:-base}; do for c in 3 5; do
+        TAILN=1 step ftime_${v}_c${c}_$r 120 tools/fold_time_$v $c
+      done; done; done ;;
     xab)
       TAILN=12 step xab_$TAG 300 python3 tools/exchange_ab.py ;;
     ptest)

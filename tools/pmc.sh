@@ -37,4 +37,7 @@ pass lds SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_SALU SQ_INSTS_SMEM SQ_WAIT_I
 pass tcc TCC_HIT_sum TCC_MISS_sum
 cpass calib_fetch FETCH_SIZE
 cpass calib_write WRITE_SIZE
-python3 tools/traffic.py "$OUT" --docs ${DOCS:-1048576} > "$OUT/summary.txt" && cat "$OUT/summary.txt"
+# the bench's exchange shares one key column between its outputs unless BENCH_ARGS has --own-keys
+case "${BENCH_ARGS:-}" in *--own-keys*) SK=0 ;; *) SK=1 ;; esac
+python3 tools/traffic.py "$OUT" --docs ${DOCS:-1048576} --config ${CONFIG:-2} --kernel "${KERNEL:-join_wave_kernel}" \
+  --shared-keys $SK --emit > "$OUT/summary.txt" && cat "$OUT/summary.txt"

@@ -42,6 +42,7 @@ def main():
     ap.add_argument("--emit", action="store_true")
     ap.add_argument("--config", type=int, default=2)
     ap.add_argument("--kernel", default="join_wave_kernel")
+    ap.add_argument("--shared-keys", type=int, default=0, help="exchange runs: the two outputs shared one key column")
     a = ap.parse_args()
     out, calib = {}, {}
     for sub in sorted(os.listdir(a.dir)):
@@ -65,6 +66,8 @@ def main():
     j = out.get(jk, {})
     res = {"docs": a.docs, "config": a.config, "kernel": jk, "exchange": jk.startswith("join") and jk.endswith("true>"),
            "fetch_correction": fcorr, "write_correction": wcorr}
+    if res["exchange"]:
+        res["shared_keys"] = bool(a.shared_keys)
     if j.get("FETCH_SIZE") is not None and j.get("WRITE_SIZE") is not None:
         rd = j["FETCH_SIZE"] * 1024 * (fcorr or 1.0)
         wr = j["WRITE_SIZE"] * 1024 * (wcorr or 1.0)
@@ -76,7 +79,8 @@ def main():
         # profiles/traffic.json: one entry per (config, docs, kernel); bench.py picks its own
         path = "profiles/traffic.json"
         table = json.load(open(path)) if os.path.exists(path) else []
-        table = [e for e in table if (e["config"], e["docs"], e["kernel"]) != (res["config"], res["docs"], res["kernel"])]
+        ident = lambda e: (e["config"], e["docs"], e["kernel"], e.get("shared_keys", False))  # noqa: E731
+        table = [e for e in table if ident(e) != ident(res)]
         table.append(res)
         json.dump(table, open(path, "w"), indent=1)
 
