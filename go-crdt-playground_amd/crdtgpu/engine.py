@@ -175,10 +175,12 @@ class Engine:
               "crdt_awset_join_batch")
         return out
 
-    def exchange(self, a: AWSetBatch, b: AWSetBatch):
+    def exchange(self, a: AWSetBatch, b: AWSetBatch, shared_keys: bool = False):
+        """Host buffers: (a <- b, b <- a); shared_keys: both outputs use one key column."""
         a, b = a.numpy(), b.numpy()
         slots = int(a.offsets[-1]) + int(b.offsets[-1])
-        o1, o2 = OutBuffers(a.n_docs, a.R, slots), OutBuffers(a.n_docs, a.R, slots)
+        o1 = OutBuffers(a.n_docs, a.R, slots)
+        o2 = OutBuffers(a.n_docs, a.R, slots, shared_keys=o1 if shared_keys else None)
         ca, cb, c1, c2 = a.c(), b.c(), o1.c(), o2.c()
         check(self._lib.crdt_awset_exchange_batch(self._ctx, ctypes.byref(ca), ctypes.byref(cb), ctypes.byref(c1),
                                                   ctypes.byref(c2)), "crdt_awset_exchange_batch")

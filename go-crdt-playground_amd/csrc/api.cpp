@@ -843,11 +843,12 @@ crdt_awset_out stage_out(Stager& st, uint32_t n_docs, uint32_t R, size_t slots) 
     return o;
 }
 
+// keys = false: the key column is shared with an output fetched before (exchange)
 int fetch_out(const crdt_awset_out* h, const crdt_awset_out& d, uint32_t n_docs, uint32_t R, size_t slots,
-              hipStream_t s) {
+              hipStream_t s, bool keys = true) {
     int rc = get(h->offsets, d.offsets, (size_t)n_docs + 1, s);
     if (rc == CRDT_OK) rc = get(h->counts, d.counts, n_docs, s);
-    if (rc == CRDT_OK) rc = get(h->keys, d.keys, slots, s);
+    if (rc == CRDT_OK && keys) rc = get(h->keys, d.keys, slots, s);
     if (rc == CRDT_OK) rc = get(h->actors, d.actors, slots, s);
     if (rc == CRDT_OK) rc = get(h->counters, d.counters, slots, s);
     if (rc == CRDT_OK) rc = get(h->vv, d.vv, (size_t)n_docs * R, s);
@@ -871,8 +872,8 @@ int order_gate(crdt_ctx* ctx, int rc) {
 // only the live entries, gathered on the device at offsets = the prefix sums
 // of the counts, so PCIe moves live entries only.
 int fetch_merge_out(crdt_ctx* ctx, Stager& st, const crdt_awset_out* h, const crdt_awset_out& d, uint32_t n,
-                    uint32_t R, size_t slots) {
-    if (!ctx->pack_outputs) return fetch_out(h, d, n, R, slots, ctx->stream);
+                    uint32_t R, size_t slots, bool keys = true) {
+    if (!ctx->pack_outputs) return fetch_out(h, d, n, R, slots, ctx->stream, keys);
     int rc = get(h->counts, d.counts, n, ctx->stream);
     if (rc == CRDT_OK && hipStreamSynchronize(ctx->stream) != hipSuccess) rc = CRDT_E_HIP;
     if (rc != CRDT_OK) return rc;
@@ -891,7 +892,7 @@ int fetch_merge_out(crdt_ctx* ctx, Stager& st, const crdt_awset_out* h, const cr
                            nullptr};
     if (st.rc != CRDT_OK) return st.rc;
     rc = hip_err(launch_pack_out(view(&d), poff, n, view(&p), (uint32_t)ctx->n_cu, ctx->stream));
-    if (rc == CRDT_OK) rc = get(h->keys, p.keys, tot, ctx->stream);
+    if (rc == CRDT_OK && keys) rc = get(h->keys, p.keys, tot, ctx->stream);
     if (rc == CRDT_OK) rc = get(h->actors, p.actors, tot, ctx->stream);
     if (rc == CRDT_OK) rc = get(h->counters, p.counters, tot, ctx->stream);
     if (rc == CRDT_OK) rc = get(h->vv, d.vv, (size_t)n * R, ctx->stream);
@@ -1010,6 +1011,9 @@ int crdt_awset_exchange_batch(crdt_ctx* ctx, const crdt_awset_batch* a, const cr
     crdt_awset_out o1 = stage_out(st, a->n_docs, a->R, slots);
     crdt_awset_out o2 = stage_out(st, a->n_docs, a->R, slots);
     if (st.rc != CRDT_OK) return st.rc;
+    // host outputs sharing one key column: one device column, written and fetched once
+    const bool share = out_ab->keys == out_ba->keys;
+    if (share) o2.keys = o1.keys;
     pc.mark("stage issued");
     rc = check_order(ctx, da.offsets, da.counts, da.n_docs, da.keys);
     if (rc == CRDT_OK) rc = check_order(ctx, db.offsets, db.counts, db.n_docs, db.keys);
@@ -1019,7 +1023,7 @@ int crdt_awset_exchange_batch(crdt_ctx* ctx, const crdt_awset_batch* a, const cr
     pc.mark("kernels issued");
     if (rc == CRDT_OK) rc = fetch_merge_out(ctx, st, out_ab, o1, a->n_docs, a->R, slots);
     pc.mark("fetch a<-b issued (after a sync)");
-    if (rc == CRDT_OK) rc = fetch_merge_out(ctx, st, out_ba, o2, a->n_docs, a->R, slots);
+    if (rc == CRDT_OK) rc = fetch_merge_out(ctx, st, out_ba, o2, a->n_docs, a->R, slots, !share);
     pc.mark("fetch b<-a issued (after a sync)");
     const int sync = crdt_ctx_sync(ctx, ctx->stream);
     pc.mark("synced");

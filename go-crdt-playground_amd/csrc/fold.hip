@@ -700,6 +700,15 @@ struct DocMeta {
 #ifndef CRDT_FOLD_NO_STORES
 #define CRDT_FOLD_NO_STORES 0
 #endif
+#ifndef CRDT_FOLD_PURE_CHUNKS
+#define CRDT_FOLD_PURE_CHUNKS 0
+#endif
+#ifndef CRDT_FOLD_PAD_VALU
+#define CRDT_FOLD_PAD_VALU 0
+#endif
+#ifndef CRDT_FOLD_PAD_SALU
+#define CRDT_FOLD_PAD_SALU 0
+#endif
 #ifndef CRDT_FOLD_WAVES
 #define CRDT_FOLD_WAVES 2
 #endif
@@ -833,6 +842,23 @@ __global__ __launch_bounds__(fold_waves<DELTA>() * 64) __attribute__((amdgpu_wav
     auto prefetch = [&](FoldPref<NCH, VCH>& P, const DocMeta& q) {
 #pragma unroll
         for (int c = 0; c < NCH; ++c) {
+#if CRDT_FOLD_PURE_CHUNKS
+            // a chunk inside one region (the document's entries, the source
+            // entries or the tombstones): buffer loads from that region's
+            // scalar base, no per-lane pointer select
+            const uint32_t lo = c * 64u, hi = lo + 64u;
+            const bool pure_d = hi <= q.n, pure_e = lo >= q.n && hi <= q.n + q.E;
+            if (lo < q.N && (pure_d || pure_e)) {
+                const uint32_t r0 = pure_d ? q.doff + lo : q.e0 + (lo - q.n);
+                const uint32_t o8 = lane * 8u, o4 = lane * 4u;
+                const rsrc_t rk = make_rsrc(pure_d ? dst.keys + r0 : sb.keys + r0, 512u);
+                const rsrc_t ra = make_rsrc(pure_d ? dst.actors + r0 : sb.actors + r0, 256u);
+                const rsrc_t rc = make_rsrc(pure_d ? dst.counters + r0 : sb.counters + r0, 512u);
+                P.k[c] = __builtin_bit_cast(uint64_t, __builtin_amdgcn_raw_buffer_load_b64(rk, (int)o8, 0, kAuxNT));
+                P.a[c] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(ra, (int)o4, 0, kAuxNT);
+                P.c[c] = __builtin_bit_cast(uint64_t, __builtin_amdgcn_raw_buffer_load_b64(rc, (int)o8, 0, kAuxNT));
+            } else
+#endif
             if ((uint32_t)c * 64u < q.N) {
                 uint32_t i = c * 64u + lane;
                 i = i < q.N ? i : q.N - 1u;
@@ -892,6 +918,17 @@ __global__ __launch_bounds__(fold_waves<DELTA>() * 64) __attribute__((amdgpu_wav
 #pragma unroll
         for (int c = 0; c < VCH; ++c) asm volatile("" ::"v"(P.sv[c]));
         asm volatile("" ::"v"(P.dv), "v"(P.eo), "v"(P.eo2), "v"(P.to), "v"(P.to2), "v"(P.act));
+#if CRDT_FOLD_PAD_VALU || CRDT_FOLD_PAD_SALU
+        {   // diagnostic (tools/fold_probe timing builds): N dependent VALU / SALU
+            // instructions per document -- the slope says which issue port binds
+            uint32_t pv = lane, ps = k;
+#pragma unroll
+            for (int i = 0; i < CRDT_FOLD_PAD_VALU; ++i) asm volatile("v_add_u32 %0, %0, 1" : "+v"(pv));
+#pragma unroll
+            for (int i = 0; i < CRDT_FOLD_PAD_SALU; ++i) asm volatile("s_add_u32 %0, %0, 1" : "+s"(ps));
+            err |= (pv == 0xFFFFFFFFu && ps == 0xFFFFFFFFu) ? kErrWorkspace : 0u;
+        }
+#endif
         // ---- stage document k (its loads were issued one document ago)
         uint64_t vreg = 0;              // lane r < R: V_0[r]
         uint32_t soffv = 0, toffv = 0;  // lane s: end of source s's entries / tombstones

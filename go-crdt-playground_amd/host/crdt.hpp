@@ -955,7 +955,9 @@ inline void ExchangeBatch(const std::vector<AWSet*>& as, const std::vector<AWSet
     Batch& b = join_batch(e, as, bs, "ExchangeBatch");
     const crdt_awset_batch ca = pack(b, e, false), cb = src_view(b, e);
     const size_t n = b.n_docs, slots = (size_t)b.dfirst[n] + b.sfirst[n];
-    const crdt_awset_out oab = out_arrays(e, kO_OFF, n, b.R, slots), oba = out_arrays(e, kP_OFF, n, b.R, slots);
+    const crdt_awset_out oab = out_arrays(e, kO_OFF, n, b.R, slots);
+    crdt_awset_out oba = out_arrays(e, kP_OFF, n, b.R, slots);
+    oba.keys = oab.keys;  // both directions hold the same keys at the same slots: one column, fetched once
     LastStats().pack_s = secs_since(t0);
     t0 = clk::now();
     check(crdt_awset_exchange_batch(e.ctx(), &ca, &cb, &oab, &oba), "crdt_awset_exchange_batch");

@@ -366,6 +366,10 @@ func (e *Engine) ExchangeBatch(as, bs []*crdt.AWSet) error {
 	if a.err != nil {
 		return a.err
 	}
+	// both directions hold the same keys at the same slots: one key column,
+	// written and downloaded once (include/crdtgpu.h, crdt_awset_exchange_*)
+	oba.e.keys = oab.e.keys
+	oba.c.keys = oab.c.keys
 	if rc := C.crdt_awset_exchange_batch(e.ctx, &ca, &cb, &oab.c, &oba.c); rc != 0 {
 		return errOf("crdt_awset_exchange_batch", rc)
 	}

@@ -180,7 +180,11 @@ int crdt_awset_join_async(crdt_ctx* ctx, const crdt_awset_batch* dst, const crdt
 /* Anti-entropy exchange: out_ab[d] = a[d] <- b[d] AND out_ba[d] = b[d] <- a[d]
  * (two (*AWSet).Merge calls per doc, awset.go:103-161) from ONE read of both
  * states.  Both directions keep the same keys at the same slots; only a
- * common key's dot differs (the src dot wins, awset.go:142). */
+ * common key's dot differs (the src dot wins, awset.go:142).  So the two
+ * outputs may share one key column: out_ba->keys == out_ab->keys is allowed
+ * and writes the keys once; every other output array must be distinct.
+ * (crdt_awset_exchange_batch: the same for host outputs -- the shared column
+ * is also downloaded once.) */
 int crdt_awset_exchange_async(crdt_ctx* ctx, const crdt_awset_batch* a, const crdt_awset_batch* b,
                               const crdt_awset_out* out_ab, const crdt_awset_out* out_ba, void* stream);
 int crdt_awset_fold_async(crdt_ctx* ctx, int mode, const crdt_awset_batch* dst, const crdt_src_batch* srcs,

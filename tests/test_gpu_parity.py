@@ -684,6 +684,29 @@ def test_exchange_config2_full_size(eng, torch, stage, shared):
     assert_same_all(host_out(oba, torch), want, n, 2)
 
 
+@pytest.mark.parametrize("packed", [0, 1])
+def test_exchange_batch_shared_key_column(eng, packed):
+    """crdt_awset_exchange_batch with host outputs sharing one key column (the
+    C++ mirror's and the Go binding's ExchangeBatch): fetched once, both
+    directions exact (wave, tile and block paths; packed and slot layouts)."""
+    rng = random.Random(44)
+    R = 3
+    a, b = join_case(rng, 300, R, lambda: rng.choice([0, 5, 64, 65, 300, 2000]), 5000, 9)
+    eng.set_option("pack_batch_outputs", packed)
+    try:
+        o1, o2 = eng.exchange(a, b, shared_keys=True)
+    finally:
+        eng.set_option("pack_batch_outputs", 0)
+    assert o1.keys is o2.keys
+    rc, w1 = oracle.join(a, b)
+    assert rc == 0
+    rc, w2 = oracle.join(b, a)
+    assert rc == 0
+    for got, want in ((o1, w1), (o2, w2)):  # per document (a packed output has its own slot bounds)
+        for d in range(a.n_docs):
+            assert out_doc(got, d, R) == out_doc(want, d, R), d
+
+
 @pytest.mark.parametrize("stage", [1, 0])
 def test_exchange_shared_key_column_mixed_sizes(eng, torch, stage):
     """One shared key column for both exchange outputs on the wave, tile and

@@ -18,6 +18,22 @@
 
 using namespace crdt;
 
+// order-independent checksum of an output (every slot; the buffers are zeroed
+// first, so slack slots hash the same in every build): variants of the fold
+// must print the same value
+__global__ void checksum_kernel(const uint32_t* counts, const uint64_t* vv, size_t n_vv, const uint64_t* keys,
+                                const uint32_t* actors, const uint64_t* ctrs, size_t slots, uint32_t n,
+                                unsigned long long* out) {
+    unsigned long long h = 0;
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < slots; i += stride)
+        h += (keys[i] * 0x9E3779B97F4A7C15ull) ^ (ctrs[i] * 0xC2B2AE3D27D4EB4Full) ^ ((uint64_t)actors[i] << 17) ^ i;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n_vv; i += stride)
+        h += (vv[i] + 0x165667B19E3779F9ull) * (i + 1);
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += stride) h += (uint64_t)counts[i] << (i & 31);
+    atomicAdd(out, h);
+}
+
 #define CK(x)                                                                        \
     do {                                                                             \
         hipError_t e_ = (x);                                                         \
@@ -56,6 +72,11 @@ int main(int argc, char** argv) {
         CK(launch_gen_delta(0x5EED, n, R, M, D, S, 0));
     const size_t oslots = (size_t)n * nd + ns * E;
     OutView O = make_out(n, R, oslots);
+    CK(hipMemset(O.keys, 0, oslots * 8));
+    CK(hipMemset(O.counters, 0, oslots * 8));
+    CK(hipMemset(O.actors, 0, oslots * 4));
+    CK(hipMemset(O.vv, 0, (size_t)n * R * 8));
+    CK(hipMemset(O.counts, 0, (size_t)n * 4));
     uint32_t* ws = dalloc<uint32_t>(64);
     CK(hipMemset(ws, 0, 64 * 4));
     Work wk{ws + 16, ws, ws + 1, dalloc<uint32_t>(n), ws + 8, dalloc<uint32_t>(n), ws + 2};
@@ -89,6 +110,13 @@ int main(int argc, char** argv) {
 #endif
     uint32_t status = 0;
     CK(hipMemcpy(&status, ws + 16, 4, hipMemcpyDeviceToHost));
+    unsigned long long* dsum = dalloc<unsigned long long>(1);
+    CK(hipMemset(dsum, 0, 8));
+    hipLaunchKernelGGL(checksum_kernel, dim3(4096), dim3(256), 0, 0, O.counts, O.vv, (size_t)n * R, O.keys, O.actors,
+                       O.counters, oslots, n, dsum);
+    unsigned long long hsum = 0;
+    CK(hipMemcpy(&hsum, dsum, 8, hipMemcpyDeviceToHost));
+    printf("output checksum %016llx\n", hsum);
     const char* names[16] = {"stage", "prefetch", "schedule", "classify", "noop+keep", "sort-group", "write",
                              "sort|walk-span", "elem-flags|walk-rows", "dot-scan+gaps|walk-bits", "step-of-tuple", "cmax",
                              "meta-next", "noop", "", "doc-loop"};

@@ -13,6 +13,8 @@
 #   pmc      PMC passes (tools/pmc.sh; one rocprofv3 --pmc run per counter group)
 #   probe    stamped fold probe (tools/fold_probe, built on the CPU side first)
 #   multi    the two-process device-summary test alone
+#   layout   HBM rate vs workgroup -> address mapping (tools/bw_layout)
+#   btrace   boundary_bench (C++ mirror ExchangeBatch) with per-phase host stamps, then under a HIP API trace
 #   xab      config-2 exchange store forms A/B (tools/exchange_ab.py)
 #   ptest    pytest -m gpu on $PTEST (a -k expression)
 #   ftime    fold timing builds tools/fold_time_$FTIME (space-separated variant names), interleaved, configs 3 and 5
@@ -51,6 +53,12 @@ for r in "$@"; do
       for r in 1 2 3; do for v in ${FTIME:-base}; do for c in 3 5; do
         TAILN=1 step ftime_${v}_c${c}_$r 120 tools/fold_time_$v $c
       done; done; done ;;
+    layout)
+      TAILN=60 step layout_$TAG 300 tools/bw_layout ;;
+    btrace)
+      TAILN=30 step bplain_$TAG 200 env CRDT_TRACE_STAGE=1 go-crdt-playground_amd/host/build/boundary_bench 65536
+      CRDT_TRACE_STAGE=1 TAILN=10 step btrace_$TAG 300 rocprofv3 --hip-trace --memory-copy-trace --kernel-trace --stats \
+        --output-format csv -d gpurun_out/btrace_$TAG -o run -- go-crdt-playground_amd/host/build/boundary_bench 65536 ;;
     xab)
       TAILN=12 step xab_$TAG 300 python3 tools/exchange_ab.py ;;
     ptest)
