@@ -60,14 +60,18 @@ def box_probe(eng, dev, nbytes=2 << 30, reps=10):
     a.fill_(0x5A)
     torch.cuda.synchronize()
     kinds = {"read": abi.CRDT_PROBE_READ, "write_nt": abi.CRDT_PROBE_WRITE, "write_plain": abi.CRDT_PROBE_WRITE_PLAIN,
-             "copy_nt": abi.CRDT_PROBE_COPY, "copy_plain": abi.CRDT_PROBE_COPY_PLAIN}
+             "copy_nt": abi.CRDT_PROBE_COPY, "copy_plain": abi.CRDT_PROBE_COPY_PLAIN,
+             "mix_nt": abi.CRDT_PROBE_MIX, "mix_plain": abi.CRDT_PROBE_MIX_PLAIN}
     variants = {}
-    for bpc in (8, 16, 32):
-        eng.set_option("probe_blocks_per_cu", bpc)
-        for name, kind in kinds.items():
-            src = None if name.startswith("write") else a
-            variants["%s@%d" % (name, bpc)] = eng.bw_probe(kind, src, b, nbytes, reps)
+    for slab in (0, 1):  # grid-stride sweep; one contiguous slab per workgroup
+        eng.set_option("probe_slab", slab)
+        for bpc in (8, 16, 32):
+            eng.set_option("probe_blocks_per_cu", bpc)
+            for name, kind in kinds.items():
+                src = None if name.startswith("write") else a
+                variants["%s@%d%s" % (name, bpc, "/slab" if slab else "")] = eng.bw_probe(kind, src, b, nbytes, reps)
     eng.set_option("probe_blocks_per_cu", 16)
+    eng.set_option("probe_slab", 0)
     del a, b
     torch.cuda.synchronize()
     torch.cuda.empty_cache()
@@ -76,7 +80,7 @@ def box_probe(eng, dev, nbytes=2 << 30, reps=10):
         return max(v for k, v in variants.items() if k.startswith(prefix))
 
     return {"bytes": nbytes, "reps": reps, "read_gbs": best("read"), "write_gbs": best("write"),
-            "copy_gbs": best("copy"), "sclk_mhz": eng.clock_probe(), "variants": variants}
+            "copy_gbs": best("copy"), "mix_gbs": best("mix"), "sclk_mhz": eng.clock_probe(), "variants": variants}
 
 
 def _np_copy(t, n, dt):
@@ -494,6 +498,8 @@ def _box_fields(roof, box):
         roof["box_write_gbs"] = box["write_gbs"]
         roof["box_copy_gbs"] = box["copy_gbs"]
         roof["frac_vs_box"] = a / box["copy_gbs"] if box["copy_gbs"] else None
+        roof["box_mix_gbs"] = box.get("mix_gbs")
+        roof["frac_vs_box_mix"] = a / box["mix_gbs"] if box.get("mix_gbs") else None
         roof["box_sclk_mhz"] = box.get("sclk_mhz")
 
 
@@ -810,8 +816,11 @@ def main():
         result["config"]["collective"] = collective
     if box:
         result["box_probe"] = dict(box, what="crdt_bw_probe on this box before timing: streaming read (16 B/lane), "
-                                             "write and copy (read+write bytes), best of nt/plain stores and 8/16/32 "
-                                             "workgroups per CU; roofline.frac_vs_box = achieved / copy_gbs; sclk_mhz: "
+                                             "write, copy (read+write bytes) and a 3:4 read:write mix (all bytes), "
+                                             "best of nt/plain stores, 8/16/32 workgroups per CU and two block orders "
+                                             "(grid-stride; one contiguous slab per workgroup, '/slab', which reaches "
+                                             "the box's ceiling); roofline.frac_vs_box = achieved / copy_gbs, "
+                                             "frac_vs_box_mix = achieved / mix_gbs; sclk_mhz: "
                                              "shader clock under an all-CU integer load (crdt_clock_probe)")
     if legs:
         result["legs"] = {}

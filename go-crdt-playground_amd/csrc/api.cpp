@@ -16,8 +16,8 @@
 
 namespace crdt {
 hipError_t launch_join(const BatchView& dst, const BatchView& src, const OutView& out, const OutView* out2,
-                       const Work& wk, uint32_t docs_per_wave, bool nt_stores, bool stage_stores, uint32_t block_grid,
-                       bool no_large,
+                       const Work& wk, uint32_t docs_per_wave, bool nt_stores, bool stage_stores, uint32_t slab_blocks,
+                       uint32_t block_grid, bool no_large,
                        const TileWork* tw, uint32_t n_cu, hipStream_t stream);
 hipError_t launch_fold(int mode, const BatchView& dst, const SrcView& sb, const OutView& out, const Scratch& scr,
                        const Work& wk, uint32_t block_grid, bool lean_first, hipStream_t stream);
@@ -60,7 +60,7 @@ hipError_t launch_gen_zipf(uint64_t seed, uint32_t n_docs, const uint32_t* offse
                            const OutView& B, hipStream_t stream);
 uint32_t host_zipf_doc_size(uint64_t seed, uint32_t d);
 hipError_t launch_clock_probe(uint64_t* out, uint32_t n_cu, hipStream_t stream);
-hipError_t launch_probe(int kind, const void* a, void* b, size_t n16, uint32_t n_cu, uint32_t blocks_per_cu,
+hipError_t launch_probe(int kind, const void* a, void* b, size_t n16, uint32_t n_cu, uint32_t blocks_per_cu, bool slab,
                         hipStream_t stream);
 }  // namespace crdt
 
@@ -127,8 +127,10 @@ struct crdt_ctx {
     uint32_t join_docs_per_wave = 8;          // crdt_ctx_set_option("join_docs_per_wave")
     bool join_nt_stores = true;               // crdt_ctx_set_option("join_nt_stores")
     bool join_stage_stores = true;            // crdt_ctx_set_option("join_stage_stores")
+    uint32_t join_slab_per_cu = 0;            // crdt_ctx_set_option("join_slab_blocks_per_cu"): 0 = blocks in order
     bool fold_lean_first = true;              // crdt_ctx_set_option("fold_lean_first")
     uint32_t probe_blocks_per_cu = 16;        // crdt_ctx_set_option("probe_blocks_per_cu")
+    bool probe_slab = false;                  // crdt_ctx_set_option("probe_slab")
     bool pack_outputs = false;                // crdt_ctx_set_option("pack_batch_outputs")
     // staging for the *_batch host path
     DevBuf stage[32];
@@ -365,6 +367,10 @@ int crdt_ctx_set_option(crdt_ctx* ctx, const char* name, int64_t value) {
         ctx->pack_outputs = value != 0;
         return CRDT_OK;
     }
+    if (!strcmp(name, "probe_slab")) {  // bandwidth probes: one contiguous slab per workgroup
+        ctx->probe_slab = value != 0;
+        return CRDT_OK;
+    }
     if (!strcmp(name, "probe_blocks_per_cu")) {
         if (value < 1 || value > 64) return CRDT_E_INVALID;
         ctx->probe_blocks_per_cu = (uint32_t)value;
@@ -380,6 +386,11 @@ int crdt_ctx_set_option(crdt_ctx* ctx, const char* name, int64_t value) {
     }
     if (!strcmp(name, "join_stage_stores")) {
         ctx->join_stage_stores = value != 0;
+        return CRDT_OK;
+    }
+    if (!strcmp(name, "join_slab_blocks_per_cu")) {  // slab order of the wave kernel's blocks (SlabMap G per CU)
+        if (value < 0 || value > 64) return CRDT_E_INVALID;
+        ctx->join_slab_per_cu = (uint32_t)value;
         return CRDT_OK;
     }
     return CRDT_E_INVALID;
@@ -441,7 +452,8 @@ static int join_common(crdt_ctx* ctx, const crdt_awset_batch* dst, const crdt_aw
     OutView o2v;
     if (out2) o2v = view(out2);
     rc = hip_err(launch_join(view(dst), view(src), view(out), out2 ? &o2v : nullptr, make_work(ctx),
-                             ctx->join_docs_per_wave, ctx->join_nt_stores, ctx->join_stage_stores, block_grid(ctx), no_large,
+                             ctx->join_docs_per_wave, ctx->join_nt_stores, ctx->join_stage_stores,
+                             ctx->join_slab_per_cu * (uint32_t)ctx->n_cu, block_grid(ctx), no_large,
                              tiles ? &tw : nullptr, (uint32_t)ctx->n_cu, s));
     return leave(ctx, s, cap, rc);
 }
@@ -646,10 +658,10 @@ int crdt_bw_probe(crdt_ctx* ctx, int kind, const void* a, void* b, size_t bytes,
     rc = hip_err(hipEventCreate(&e0));
     if (rc == CRDT_OK) rc = hip_err(hipEventCreate(&e1));
     // one untimed launch (first touch, clocks up), then reps timed back to back
-    if (rc == CRDT_OK) rc = hip_err(launch_probe(kind, a, b, n16, (uint32_t)ctx->n_cu, ctx->probe_blocks_per_cu, s));
+    if (rc == CRDT_OK) rc = hip_err(launch_probe(kind, a, b, n16, (uint32_t)ctx->n_cu, ctx->probe_blocks_per_cu, ctx->probe_slab, s));
     if (rc == CRDT_OK) rc = hip_err(hipEventRecord(e0, s));
     for (int r = 0; r < reps && rc == CRDT_OK; ++r)
-        rc = hip_err(launch_probe(kind, a, b, n16, (uint32_t)ctx->n_cu, ctx->probe_blocks_per_cu, s));
+        rc = hip_err(launch_probe(kind, a, b, n16, (uint32_t)ctx->n_cu, ctx->probe_blocks_per_cu, ctx->probe_slab, s));
     if (rc == CRDT_OK) rc = hip_err(hipEventRecord(e1, s));
     if (rc == CRDT_OK) rc = hip_err(hipEventSynchronize(e1));
     float ms = 0.f;

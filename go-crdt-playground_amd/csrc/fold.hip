@@ -23,6 +23,39 @@
 
 namespace crdt {
 
+// ---- build options (tools/fold_probe.hip timing builds override them) ----
+// Measured on config 3 / 5 with timing builds, three interleaved rounds each,
+// outputs checksummed equal (round 4):
+//  * CRDT_FOLD_PAD_VALU / _SALU = 200 (diagnostic: 200 dependent VALU or SALU
+//    instructions per document): +8 % / +7 % on config 3, +20 % / +26 % on
+//    config 5 -- config 5 (6 waves per SIMD) is near issue-bound, config 3
+//    (4 waves per SIMD) is bound by its per-document dependent chain;
+//  * CRDT_FOLD_PURE_CHUNKS (buffer loads for a chunk inside one region instead
+//    of per-lane pointer selects): no change (-0.5 % / +1 %), off;
+//  * branch-free slot walks (every lane issues the atomics and reads, no
+//    per-lane branch): +8 % / +5 %, dropped; branch-free staging (below): -2 %
+//    on config 5, kept.
+// 1: survivors staged through LDS and written as contiguous lines -- measured
+// 4 % slower on config 3 and 5 % on config 5 (tools/fold_probe.hip timing
+// builds, three interleaved rounds), so off: each lane stores its own
+// survivors at their slots.  (CRDT_FOLD_NO_STORES, a diagnostic bound that
+// writes nothing, is only 4 % faster: the folds are not bound by their stores.)
+#ifndef CRDT_FOLD_STAGE_STORES
+#define CRDT_FOLD_STAGE_STORES 0
+#endif
+#ifndef CRDT_FOLD_NO_STORES
+#define CRDT_FOLD_NO_STORES 0
+#endif
+#ifndef CRDT_FOLD_PURE_CHUNKS
+#define CRDT_FOLD_PURE_CHUNKS 0
+#endif
+#ifndef CRDT_FOLD_PAD_VALU
+#define CRDT_FOLD_PAD_VALU 0
+#endif
+#ifndef CRDT_FOLD_PAD_SALU
+#define CRDT_FOLD_PAD_SALU 0
+#endif
+
 // ---- the fold restated per key ---------------------------------------------
 // A key's fate over the whole fold depends only on its own tuples (its dot in
 // the document, its entry in each source, its tombstone in each source) and on
@@ -453,6 +486,11 @@ __device__ __forceinline__ bool dense_delta_walk(Smem& m, const uint64_t (&key)[
     uint32_t lo = ~0u, hi = 0u;
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
+        if ((uint32_t)c * 64u >= N) {  // a chunk past the document's tuples (wave-uniform): nothing kept
+            kept[c] = false;
+            a[c] = 0;
+            continue;
+        }
         const uint32_t i = c * 64u + lane;
         const uint32_t j = step[c] & 63u;
         const bool fj = (full_mask >> j) & 1ull, nj = (noop_mask >> j) & 1ull, f = (flag >> c) & 1u;
@@ -689,26 +727,6 @@ struct DocMeta {
     uint32_t d, doff, slots, n, s0, ms, e0, E, t0, X, N, big;
 };
 
-// 1: survivors staged through LDS and written as contiguous lines -- measured
-// 4 % slower on config 3 and 5 % on config 5 (tools/fold_probe.hip timing
-// builds, three interleaved rounds), so off: each lane stores its own
-// survivors at their slots.  (CRDT_FOLD_NO_STORES, a diagnostic bound that
-// writes nothing, is only 4 % faster: the folds are not bound by their stores.)
-#ifndef CRDT_FOLD_STAGE_STORES
-#define CRDT_FOLD_STAGE_STORES 0
-#endif
-#ifndef CRDT_FOLD_NO_STORES
-#define CRDT_FOLD_NO_STORES 0
-#endif
-#ifndef CRDT_FOLD_PURE_CHUNKS
-#define CRDT_FOLD_PURE_CHUNKS 0
-#endif
-#ifndef CRDT_FOLD_PAD_VALU
-#define CRDT_FOLD_PAD_VALU 0
-#endif
-#ifndef CRDT_FOLD_PAD_SALU
-#define CRDT_FOLD_PAD_SALU 0
-#endif
 #ifndef CRDT_FOLD_WAVES
 #define CRDT_FOLD_WAVES 2
 #endif
@@ -934,10 +952,14 @@ __global__ __launch_bounds__(fold_waves<DELTA>() * 64) __attribute__((amdgpu_wav
         uint32_t soffv = 0, toffv = 0;  // lane s: end of source s's entries / tombstones
         if (!cur.big) {
             const uint32_t N = cur.N, msR = cur.ms * R;
+            // Whole chunks are written (wave-uniform guards only, no per-lane
+            // branch: each divergent branch costs scalar exec-mask work): the
+            // lanes past N store a copy of the last tuple (the prefetch
+            // clamps), which nothing reads.
 #pragma unroll
             for (int c = 0; c < NCH; ++c) {
                 const uint32_t i = c * 64u + lane;
-                if ((uint32_t)c * 64u < N && i < N) {
+                if ((uint32_t)c * 64u < N) {
                     m.tk[i] = P.k[c];
                     m.ta[i] = P.a[c];
                     m.tc[i] = P.c[c];
@@ -946,22 +968,25 @@ __global__ __launch_bounds__(fold_waves<DELTA>() * 64) __attribute__((amdgpu_wav
 #pragma unroll
             for (int c = 0; c < VCH; ++c) {
                 const uint32_t i = c * 64u + lane;
-                if ((uint32_t)c * 64u < msR && i < msR) m.svv[i] = P.sv[c];
+                if constexpr (Smem::VCAP >= 64 * VCH) {  // whole chunks fit: the words past ms*R are never read
+                    if ((uint32_t)c * 64u < msR) m.svv[i] = P.sv[c];
+                } else {
+                    if ((uint32_t)c * 64u < msR && i < msR) m.svv[i] = P.sv[c];
+                }
             }
             const uint32_t nso = from_next_lane(rl(P.eo2, 0), P.eo);
             soffv = nso - cur.e0;
-            if (lane <= cur.ms) m.soff[lane] = P.eo - cur.e0;
-            if (lane == 0 && cur.ms >= 64) m.soff[64] = P.eo2 - cur.e0;
+            // per-source words of every lane (MCAP = 64: lanes past ms write words no step reads)
+            m.soff[lane] = P.eo - cur.e0;
+            if (cur.ms >= 64 && lane == 0) m.soff[64] = P.eo2 - cur.e0;
             if (tombs) {
                 const uint32_t nto = from_next_lane(rl(P.to2, 0), P.to);
                 toffv = nto - cur.t0;
             }
-            if (lane < cur.ms) {
-                m.sact[lane] = P.act;
-                m.anye[lane] = 0;
-                m.anyt[lane] = 0;
-            }
-            if (lane < Smem::NCAP / 4) reinterpret_cast<uint32_t*>(m.smark)[lane] = 0u;
+            m.sact[lane] = P.act;
+            m.anye[lane] = 0;
+            m.anyt[lane] = 0;
+            reinterpret_cast<uint32_t*>(m.smark)[lane & (Smem::NCAP / 4 - 1)] = 0u;
             wave_sync();
             // Source s's tuples end at soffv / toffv (nondecreasing in s): mark
             // s + 1 at that position (the last source ending there), so a tuple's

@@ -239,7 +239,7 @@ __device__ __forceinline__ void join_doc(JoinWaveSmem<WAVES>& sm, uint32_t w, co
 // vmcnt waits count exactly and the prefetch stays in flight.
 template <int WAVES, int K, int AUX, bool EXCH, bool STG>
 __global__ __launch_bounds__(WAVES * 64) void join_wave_kernel(BatchView dst, BatchView src, OutView out, OutView out2,
-                                                               Work wk, uint32_t no_large) {
+                                                               Work wk, uint32_t no_large, SlabMap slabs) {
     __shared__ JoinWaveSmem<WAVES> sm;
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t w = threadIdx.x >> 6;
@@ -249,7 +249,9 @@ __global__ __launch_bounds__(WAVES * 64) void join_wave_kernel(BatchView dst, Ba
     const uint32_t end_off = dst.offsets[n_docs] + src.offsets[n_docs];
     uint32_t err = 0;
 
-    const uint32_t first = uniform(blockIdx.x * (WAVES * K) + w);
+    const uint32_t chunk = slab_chunk(slabs, blockIdx.x);
+    if (chunk == 0xFFFFFFFFu) return;
+    const uint32_t first = uniform(chunk * (WAVES * K) + w);
     if (first >= n_docs) return;
     const uint32_t cnt = min((uint32_t)K, (n_docs - first + WAVES - 1) / WAVES);
     const MetaVec mv = meta_vec_issue(dst, src, first, WAVES, lane);
@@ -347,39 +349,41 @@ constexpr int kJoinWaves = 4;
 constexpr int kBlockNT = 256;
 constexpr int kBlockIPT = 4;
 
+// slab_blocks: G of the block order (crdt_device.hpp SlabMap), 0 = in order
 template <int K, int AUX, bool EXCH, bool STG>
 static void launch_wave(const BatchView& dst, const BatchView& src, const OutView& out, const OutView& out2,
-                        const Work& wk, bool no_large, hipStream_t stream) {
+                        const Work& wk, bool no_large, uint32_t slab_blocks, hipStream_t stream) {
     const uint32_t per_block = kJoinWaves * K;
-    const uint32_t grid = (dst.n_docs + per_block - 1) / per_block;
-    hipLaunchKernelGGL((join_wave_kernel<kJoinWaves, K, AUX, EXCH, STG>), dim3(grid), dim3(kJoinWaves * 64), 0, stream,
-                       dst, src, out, out2, wk, (uint32_t)no_large);
+    const SlabMap sm = slab_map((dst.n_docs + per_block - 1) / per_block, slab_blocks);
+    hipLaunchKernelGGL((join_wave_kernel<kJoinWaves, K, AUX, EXCH, STG>), dim3(slab_grid(sm)), dim3(kJoinWaves * 64), 0,
+                       stream, dst, src, out, out2, wk, (uint32_t)no_large, sm);
 }
 
 template <int AUX, bool EXCH, bool STG>
 static void launch_wave_k(uint32_t k, const BatchView& dst, const BatchView& src, const OutView& out,
-                          const OutView& out2, const Work& wk, bool no_large, hipStream_t stream) {
+                          const OutView& out2, const Work& wk, bool no_large, uint32_t sb, hipStream_t stream) {
     switch (k) {
-        case 1: launch_wave<1, AUX, EXCH, STG>(dst, src, out, out2, wk, no_large, stream); break;
-        case 2: launch_wave<2, AUX, EXCH, STG>(dst, src, out, out2, wk, no_large, stream); break;
-        case 4: launch_wave<4, AUX, EXCH, STG>(dst, src, out, out2, wk, no_large, stream); break;
-        case 16: launch_wave<16, AUX, EXCH, STG>(dst, src, out, out2, wk, no_large, stream); break;
-        default: launch_wave<8, AUX, EXCH, STG>(dst, src, out, out2, wk, no_large, stream); break;
+        case 1: launch_wave<1, AUX, EXCH, STG>(dst, src, out, out2, wk, no_large, sb, stream); break;
+        case 2: launch_wave<2, AUX, EXCH, STG>(dst, src, out, out2, wk, no_large, sb, stream); break;
+        case 4: launch_wave<4, AUX, EXCH, STG>(dst, src, out, out2, wk, no_large, sb, stream); break;
+        case 16: launch_wave<16, AUX, EXCH, STG>(dst, src, out, out2, wk, no_large, sb, stream); break;
+        default: launch_wave<8, AUX, EXCH, STG>(dst, src, out, out2, wk, no_large, sb, stream); break;
     }
 }
 
 template <bool EXCH, bool STG>
 static void launch_wave_ks(uint32_t k, bool nt_stores, const BatchView& dst, const BatchView& src, const OutView& out,
-                           const OutView& out2, const Work& wk, bool no_large, hipStream_t stream) {
+                           const OutView& out2, const Work& wk, bool no_large, uint32_t sb, hipStream_t stream) {
     if (nt_stores)
-        launch_wave_k<kAuxNT, EXCH, STG>(k, dst, src, out, out2, wk, no_large, stream);
+        launch_wave_k<kAuxNT, EXCH, STG>(k, dst, src, out, out2, wk, no_large, sb, stream);
     else
-        launch_wave_k<0, EXCH, STG>(k, dst, src, out, out2, wk, no_large, stream);
+        launch_wave_k<0, EXCH, STG>(k, dst, src, out, out2, wk, no_large, sb, stream);
 }
 
 // docs_per_wave: K of join_wave_kernel (1, 2, 4, 8 or 16); nt_stores: write the
 // output with non-temporal stores; stage_stores: place the survivors in LDS by
-// output slot and write whole contiguous lines (join_doc's STG); no_large: the caller promised every doc has
+// output slot and write whole contiguous lines (join_doc's STG); slab_blocks:
+// the wave kernel's block order (SlabMap G; 0 = in order); no_large: the caller promised every doc has
 // <= 64 entries per side, so the block path is not launched (a larger doc then
 // raises CRDT_E_INVALID).  out2 != nullptr: exchange -- also out2 = src <- dst.
 hipError_t launch_join_tiles(const BatchView& A, const BatchView& B, const OutView& o1, const OutView* o2,
@@ -389,20 +393,21 @@ hipError_t launch_join_tiles(const BatchView& A, const BatchView& B, const OutVi
 // (tile.hip); the per-document block kernel then only runs when the tiles
 // exceed the workspace (tw->fallback).
 hipError_t launch_join(const BatchView& dst, const BatchView& src, const OutView& out, const OutView* out2,
-                       const Work& wk, uint32_t docs_per_wave, bool nt_stores, bool stage_stores, uint32_t block_grid,
-                       bool no_large, const TileWork* tw, uint32_t n_cu, hipStream_t stream) {
+                       const Work& wk, uint32_t docs_per_wave, bool nt_stores, bool stage_stores, uint32_t slab_blocks,
+                       uint32_t block_grid, bool no_large, const TileWork* tw, uint32_t n_cu, hipStream_t stream) {
     if (dst.n_docs == 0) return hipSuccess;
     const OutView& o2 = out2 ? *out2 : out;
     if (out2) {
         if (stage_stores)
-            launch_wave_ks<true, true>(docs_per_wave, nt_stores, dst, src, out, o2, wk, no_large, stream);
+            launch_wave_ks<true, true>(docs_per_wave, nt_stores, dst, src, out, o2, wk, no_large, slab_blocks, stream);
         else
-            launch_wave_ks<true, false>(docs_per_wave, nt_stores, dst, src, out, o2, wk, no_large, stream);
+            launch_wave_ks<true, false>(docs_per_wave, nt_stores, dst, src, out, o2, wk, no_large, slab_blocks, stream);
     } else {
         if (stage_stores)
-            launch_wave_ks<false, true>(docs_per_wave, nt_stores, dst, src, out, o2, wk, no_large, stream);
+            launch_wave_ks<false, true>(docs_per_wave, nt_stores, dst, src, out, o2, wk, no_large, slab_blocks, stream);
         else
-            launch_wave_ks<false, false>(docs_per_wave, nt_stores, dst, src, out, o2, wk, no_large, stream);
+            launch_wave_ks<false, false>(docs_per_wave, nt_stores, dst, src, out, o2, wk, no_large, slab_blocks,
+                                         stream);
     }
     hipError_t e = hipGetLastError();
     if (e != hipSuccess || no_large) return e;

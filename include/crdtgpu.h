@@ -157,6 +157,11 @@ int crdt_ctx_set_max_doc_entries(crdt_ctx* ctx, uint32_t max_entries);
  *   "join_docs_per_wave"  1|2|4|8|16  documents one wavefront pipelines (default 8)
  *   "join_nt_stores"      0|1         non-temporal output stores (default 1)
  *   "probe_blocks_per_cu" 1..64       crdt_bw_probe grid (default 16)
+ *   "probe_slab"          0|1         crdt_bw_probe: one contiguous slab per workgroup
+ *                                     instead of a grid-stride sweep (default 0)
+ *   "join_stage_stores"   0|1         survivors staged in LDS, whole-line stores (default 1)
+ *   "join_slab_blocks_per_cu" 0..64   wave kernel block order: slabs of G = this x CUs
+ *                                     blocks (crdt_device.hpp SlabMap; 0 = in order)
  *   "fold_lean_first"     0|1         folds: slot-walk pass first, the rest deferred (default 1)
  *   (also "join_tile_capacity", "join_tile_shape", "join_tile_nt_stores",
  *   "join_tiles": see api.cpp)

@@ -1,8 +1,8 @@
 #!/usr/bin/env python3
-"""A/B of the config-2 exchange's store forms in ONE process, interleaved
-rounds: LDS-staged contiguous stores vs lane-scattered stores
-("join_stage_stores"), each with its own and with one shared key column for
-the two outputs.  Prints the median launch time, the HBM bytes each form
+"""A/B of the config-2 exchange's forms in ONE process, interleaved rounds:
+LDS-staged contiguous stores vs lane-scattered stores ("join_stage_stores"),
+one shared key column for the two outputs or one each, and the block order
+("join_slab_blocks_per_cu": 0 = in order; FORMS env: "stage,shared,slab;...").  Prints the median launch time, the HBM bytes each form
 writes, and whether every form's outputs equal the first form's (live entries,
 counts, VVs).  Also the box's copy and 3:4 mix probes.  GPU box only."""
 import os
@@ -28,11 +28,13 @@ o1 = OutBuffers(n, 2, 2 * n * 64, device=dev)
 o2 = OutBuffers(n, 2, 2 * n * 64, device=dev)
 o2s = OutBuffers(n, 2, 2 * n * 64, device=dev, shared_keys=o1)
 s = torch.cuda.current_stream()
-forms = [(st, sh) for st in (1, 0) for sh in (0, 1)]
+forms = [tuple(int(x) for x in f.split(",")) for f in os.environ.get(
+    "FORMS", "1,1,0;1,1,7;1,1,14;1,1,4;1,0,0;1,0,7").split(";")]
 
 
 def run(form, reps):
     eng.set_option("join_stage_stores", form[0])
+    eng.set_option("join_slab_blocks_per_cu", form[2])
     eng.exchange_async(a, b, o1, o2s if form[1] else o2, stream=s)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record(s)
@@ -77,9 +79,10 @@ for f in forms:
     med = v[len(v) // 2]
     # bytes: inputs 20 B/entry, out1 20 B/entry, out2 20 (own keys) or 12 B/entry, VVs/offsets/counts
     byt = 20 * n_in + (20 + (12 if f[1] else 20)) * n_out + n * (2 * 2 * 8 + 2 * 2 * 8 + 2 * 8 + 2 * 8)
-    print("stage=%d shared_keys=%d  median %.4f ms  min %.4f ms  %.0f GB/s algorithmic (%.3f GB)  same=%s" % (
-        f[0], f[1], med, v[0], byt / med / 1e6, byt / 1e9, same[f]))
+    print("stage=%d shared_keys=%d slab=%-2d median %.4f ms  min %.4f ms  %.0f GB/s algorithmic (%.3f GB)  same=%s" % (
+        f[0], f[1], f[2], med, v[0], byt / med / 1e6, byt / 1e9, same[f]))
 eng.set_option("join_stage_stores", 1)
+eng.set_option("join_slab_blocks_per_cu", 0)
 del o1, o2, o2s, A, B
 torch.cuda.empty_cache()
 x = torch.empty(2 << 30, dtype=torch.uint8, device=dev)

@@ -12,7 +12,10 @@
 #include <cstdlib>
 #include <vector>
 
-#include "../go-crdt-playground_amd/csrc/fold.hip"
+#ifndef FOLD_SRC  // A/B builds may compile another copy of the fold kernels
+#define FOLD_SRC "../go-crdt-playground_amd/csrc/fold.hip"
+#endif
+#include FOLD_SRC
 #include "../go-crdt-playground_amd/csrc/gen.hip"
 #include "../go-crdt-playground_amd/csrc/reduce.hip"
 

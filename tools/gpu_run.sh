@@ -14,6 +14,7 @@
 #   probe    stamped fold probe (tools/fold_probe, built on the CPU side first)
 #   multi    the two-process device-summary test alone
 #   layout   HBM rate vs workgroup -> address mapping (tools/bw_layout)
+#   bthreads boundary_bench at $BTHREADS host threads, with the box's cgroup CPU limits
 #   btrace   boundary_bench (C++ mirror ExchangeBatch) with per-phase host stamps, then under a HIP API trace
 #   xab      config-2 exchange store forms A/B (tools/exchange_ab.py)
 #   ptest    pytest -m gpu on $PTEST (a -k expression)
@@ -55,12 +56,18 @@ for r in "$@"; do
       done; done; done ;;
     layout)
       TAILN=60 step layout_$TAG 300 tools/bw_layout ;;
+    bthreads)
+      { cat /sys/fs/cgroup/cpu.max /sys/fs/cgroup/cpu.stat 2>&1; nproc; grep Cpus_allowed_list /proc/self/status; } > gpurun_out/cgroup_$TAG.log 2>&1 || true
+      for t in ${BTHREADS:-16 12 8}; do
+        TAILN=1 step bthreads_${t}_$TAG 200 env CRDT_HOST_THREADS=$t go-crdt-playground_amd/host/build/boundary_bench 65536
+      done
+      cat /sys/fs/cgroup/cpu.stat >> gpurun_out/cgroup_$TAG.log 2>&1 || true ;;
     btrace)
       TAILN=30 step bplain_$TAG 200 env CRDT_TRACE_STAGE=1 go-crdt-playground_amd/host/build/boundary_bench 65536
       CRDT_TRACE_STAGE=1 TAILN=10 step btrace_$TAG 300 rocprofv3 --hip-trace --memory-copy-trace --kernel-trace --stats \
         --output-format csv -d gpurun_out/btrace_$TAG -o run -- go-crdt-playground_amd/host/build/boundary_bench 65536 ;;
     xab)
-      TAILN=12 step xab_$TAG 300 python3 tools/exchange_ab.py ;;
+      TAILN=12 step xab_$TAG 400 python3 tools/exchange_ab.py ;;
     ptest)
       TAILN=6 step ptest_$TAG 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -k "$PTEST"
       grep -q " FAILED\| ERROR" gpurun_out/ptest_$TAG.log && { echo "tests failed"; exit 1; } ;;
