@@ -49,6 +49,9 @@ namespace crdt {
 #ifndef CRDT_FOLD_PURE_CHUNKS
 #define CRDT_FOLD_PURE_CHUNKS 0
 #endif
+#ifndef CRDT_FOLD_LDS_PAD
+#define CRDT_FOLD_LDS_PAD 0
+#endif
 #ifndef CRDT_FOLD_PAD_VALU
 #define CRDT_FOLD_PAD_VALU 0
 #endif
@@ -139,6 +142,9 @@ struct FoldSmem {
     uint8_t anyt[MCAP];              // step j has an effective tombstone
     alignas(4) uint8_t smark[NCAP];  // s + 1 where source s's entries / tombstones end (step of a tuple)
     alignas(8) uint16_t dbase[256];  // dense_sort: first sorted position of each key slot (64-bit stores)
+#if CRDT_FOLD_LDS_PAD
+    uint8_t pad[CRDT_FOLD_LDS_PAD];  // diagnostic builds: fewer waves per CU by LDS (occupancy slope)
+#endif
 };
 
 // The members reached by 64-bit LDS accesses (atomics on stag, stores on
