@@ -34,7 +34,19 @@ namespace crdt {
 //    of per-lane pointer selects): no change (-0.5 % / +1 %), off;
 //  * branch-free slot walks (every lane issues the atomics and reads, no
 //    per-lane branch): +8 % / +5 %, dropped; branch-free staging (below): -2 %
-//    on config 5, kept.
+//    on config 5, kept;
+//  * CRDT_FOLD_LDS_PAD (diagnostic: LDS padding, fewer waves per CU): config 3
+//    16 -> 14 -> 12 waves per CU costs +9 % / +35 %, config 5 24 -> 22 -> 16
+//    costs +9 % / +18 % -- both folds scale with resident waves, i.e. they are
+//    bound by each document's dependent chain, not by bytes or issue;
+//  * more waves by squeezing registers: the lean delta pass at 5 waves per SIMD
+//    (95 VGPRs, 40 spilled) +59 %, the lean AWSet pass at 7 (72 VGPRs) +13 %;
+//    counters and clocks staged as u32 (half the LDS of tc / vs / svv, the
+//    documents with a word >= 2^32 deferred) +2.5 % at the same occupancy;
+//    dropped;
+//  * tombstone check by reading a short source's <= 8 entries at once instead
+//    of binary-search probes: +8 % on config 3 (one VGPR spills); the source
+//    actors kept in a register instead of re-read from LDS: no change; dropped.
 // 1: survivors staged through LDS and written as contiguous lines -- measured
 // 4 % slower on config 3 and 5 % on config 5 (tools/fold_probe.hip timing
 // builds, three interleaved rounds), so off: each lane stores its own
