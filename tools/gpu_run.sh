@@ -15,6 +15,7 @@
 #   multi    the two-process device-summary test alone
 #   layout   HBM rate vs workgroup -> address mapping (tools/bw_layout)
 #   bthreads boundary_bench at $BTHREADS host threads, with the box's cgroup CPU limits
+#   bintr    boundary_bench with the runtime's interrupt-driven waits (default) and with polling waits
 #   btrace   boundary_bench (C++ mirror ExchangeBatch) with per-phase host stamps, then under a HIP API trace
 #   xab      config-2 exchange store forms A/B (tools/exchange_ab.py)
 #   ptest    pytest -m gpu on $PTEST (a -k expression)
@@ -62,6 +63,15 @@ for r in "$@"; do
         TAILN=1 step bthreads_${t}_$TAG 200 env CRDT_HOST_THREADS=$t go-crdt-playground_amd/host/build/boundary_bench 65536
       done
       cat /sys/fs/cgroup/cpu.stat >> gpurun_out/cgroup_$TAG.log 2>&1 || true ;;
+    bintr)
+      TAILN=1 step bintr_default_$TAG 200 env CRDT_TRACE_STAGE=1 go-crdt-playground_amd/host/build/boundary_bench 65536
+      TAILN=1 step bintr_poll_$TAG 200 env HSA_ENABLE_INTERRUPT=0 CRDT_TRACE_STAGE=1 go-crdt-playground_amd/host/build/boundary_bench 65536
+      TAILN=1 step bintr_default2_$TAG 200 env go-crdt-playground_amd/host/build/boundary_bench 65536
+      TAILN=1 step bintr_poll2_$TAG 200 env HSA_ENABLE_INTERRUPT=0 go-crdt-playground_amd/host/build/boundary_bench 65536 ;;
+    bsdma)
+      TAILN=1 step bsdma_off_$TAG 200 env HSA_ENABLE_SDMA=0 CRDT_TRACE_STAGE=1 go-crdt-playground_amd/host/build/boundary_bench 65536
+      TAILN=1 step bsdma_on_$TAG 200 env CRDT_TRACE_STAGE=1 go-crdt-playground_amd/host/build/boundary_bench 65536
+      TAILN=1 step bsdma_off2_$TAG 200 env HSA_ENABLE_SDMA=0 go-crdt-playground_amd/host/build/boundary_bench 65536 ;;
     btrace)
       TAILN=30 step bplain_$TAG 200 env CRDT_TRACE_STAGE=1 go-crdt-playground_amd/host/build/boundary_bench 65536
       CRDT_TRACE_STAGE=1 TAILN=10 step btrace_$TAG 300 rocprofv3 --hip-trace --memory-copy-trace --kernel-trace --stats \
