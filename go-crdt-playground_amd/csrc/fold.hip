@@ -44,6 +44,11 @@ namespace crdt {
 //    counters and clocks staged as u32 (half the LDS of tc / vs / svv, the
 //    documents with a word >= 2^32 deferred) +2.5 % at the same occupancy;
 //    dropped;
+//  * the lean passes defer > 15 sources before their prefetch and keep no
+//    registers for words they never load (the second offset chunk, the lean
+//    AWSet pass's second clock chunk): config 5 -1.5 %, kept; the lean AWSet
+//    pass then fits 7 waves per SIMD in 72 VGPRs (3 spilled): another -0.5 %,
+//    within noise, not taken;
 //  * tombstone check by reading a short source's <= 8 entries at once instead
 //    of binary-search probes: +8 % on config 3 (one VGPR spills); the source
 //    actors kept in a register instead of re-read from LDS: no change; dropped.
@@ -130,9 +135,11 @@ struct FoldShape {
     static constexpr int WPE = LEAN ? (DELTA ? CRDT_FOLD_LEAN_WPE : CRDT_FOLD_AWSET_LEAN_WPE)
                                     : (DELTA ? CRDT_FOLD_DELTA_WPE : CRDT_FOLD_AWSET_WPE);
     static constexpr int NCH = DELTA ? 4 : 2;
-    static constexpr int VCH = (LEAN && DELTA) ? 3 : (DELTA ? 4 : 2);
+    // the lean AWSet pass stages one chunk of clock words (sources x R <= 64;
+    // config 5: 7 x 8): two fewer prefetch registers
+    static constexpr int VCH = (LEAN && DELTA) ? 3 : (DELTA ? 4 : (LEAN ? 1 : 2));
     static constexpr int VCAP =
-        (LEAN && DELTA) ? 192 : ((DELTA && CRDT_FOLD_DELTA_WPE < 4) ? 256 : (DELTA ? 224 : 128));
+        (LEAN && DELTA) ? 192 : ((DELTA && CRDT_FOLD_DELTA_WPE < 4) ? 256 : (DELTA ? 224 : (LEAN ? 64 : 128)));
 };
 
 template <int VCAP_, int NCAP_>
@@ -828,7 +835,7 @@ __global__ __launch_bounds__(fold_waves<DELTA>() * 64) __attribute__((amdgpu_wav
     const uint32_t E_i = eo_hi - mv_eo;
     const uint32_t X_i = to_hi - mv_to;
     const bool big_i = lane < cnt && ((uint64_t)n_i + E_i + X_i > (uint64_t)Smem::NCAP ||
-                                      ms_i > (uint32_t)Smem::MCAP || ms_i * R > (uint32_t)Smem::VCAP);
+                                      ms_i > (uint32_t)(LEAN ? 15 : Smem::MCAP) || ms_i * R > (uint32_t)Smem::VCAP);
     const uint64_t bigm = ballot(big_i);
     if (big_i) {
         if (LEAN)
@@ -917,11 +924,11 @@ __global__ __launch_bounds__(fold_waves<DELTA>() * 64) __attribute__((amdgpu_wav
         P.dv = ld64(make_rsrc(dst.vv + (size_t)q.d * R, R * 8u), lane * 8u);
         const rsrc_t re = make_rsrc(sb.entry_off + q.s0, (q.ms + 1u) * 4u);
         P.eo = ld32(re, lane * 4u);
-        if (q.ms >= 64) P.eo2 = ld32(re, (64u + lane) * 4u);
+        if (!LEAN && q.ms >= 64) P.eo2 = ld32(re, (64u + lane) * 4u);
         if (tombs) {
             const rsrc_t rt = make_rsrc(sb.tomb_off + q.s0, (q.ms + 1u) * 4u);
             P.to = ld32(rt, lane * 4u);
-            if (q.ms >= 64) P.to2 = ld32(rt, (64u + lane) * 4u);
+            if (!LEAN && q.ms >= 64) P.to2 = ld32(rt, (64u + lane) * 4u);
         }
         P.act = ld32(make_rsrc(sb.src_actor + q.s0, q.ms * 4u), lane * 4u);
     };
@@ -953,7 +960,10 @@ __global__ __launch_bounds__(fold_waves<DELTA>() * 64) __attribute__((amdgpu_wav
         for (int c = 0; c < NCH; ++c) asm volatile("" ::"v"(P.k[c]), "v"(P.c[c]), "v"(P.a[c]));
 #pragma unroll
         for (int c = 0; c < VCH; ++c) asm volatile("" ::"v"(P.sv[c]));
-        asm volatile("" ::"v"(P.dv), "v"(P.eo), "v"(P.eo2), "v"(P.to), "v"(P.to2), "v"(P.act));
+        asm volatile("" ::"v"(P.dv), "v"(P.eo), "v"(P.act));
+        if constexpr (!LEAN) asm volatile("" ::"v"(P.eo2));  // (the lean passes defer > 15 sources)
+        if constexpr (DELTA) asm volatile("" ::"v"(P.to));
+        if constexpr (DELTA && !LEAN) asm volatile("" ::"v"(P.to2));
 #if CRDT_FOLD_PAD_VALU || CRDT_FOLD_PAD_SALU
         {   // diagnostic (tools/fold_probe timing builds): N dependent VALU / SALU
             // instructions per document -- the slope says which issue port binds
@@ -992,13 +1002,13 @@ __global__ __launch_bounds__(fold_waves<DELTA>() * 64) __attribute__((amdgpu_wav
                     if ((uint32_t)c * 64u < msR && i < msR) m.svv[i] = P.sv[c];
                 }
             }
-            const uint32_t nso = from_next_lane(rl(P.eo2, 0), P.eo);
+            const uint32_t nso = from_next_lane(LEAN ? 0u : rl(P.eo2, 0), P.eo);
             soffv = nso - cur.e0;
             // per-source words of every lane (MCAP = 64: lanes past ms write words no step reads)
             m.soff[lane] = P.eo - cur.e0;
             if (cur.ms >= 64 && lane == 0) m.soff[64] = P.eo2 - cur.e0;
             if (tombs) {
-                const uint32_t nto = from_next_lane(rl(P.to2, 0), P.to);
+                const uint32_t nto = from_next_lane(LEAN ? 0u : rl(P.to2, 0), P.to);
                 toffv = nto - cur.t0;
             }
             m.sact[lane] = P.act;
