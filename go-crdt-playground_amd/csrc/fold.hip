@@ -49,6 +49,10 @@ namespace crdt {
 //    AWSet pass's second clock chunk): config 5 -1.5 %, kept; the lean AWSet
 //    pass then fits 7 waves per SIMD in 72 VGPRs (3 spilled): another -0.5 %,
 //    within noise, not taken;
+//  * the lean delta pass's survivors written per slot quad inside the walk (no
+//    Emit registers) with u32 staging: 128 -> 109 VGPRs, but +7.5 % at 4 waves
+//    per SIMD, and at 5 waves (96 VGPRs, 3 spilled) still +5.6 % on config 3
+//    (+3 % config 5); dropped;
 //  * tombstone check by reading a short source's <= 8 entries at once instead
 //    of binary-search probes: +8 % on config 3 (one VGPR spills); the source
 //    actors kept in a register instead of re-read from LDS: no change; dropped.
