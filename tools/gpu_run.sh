@@ -17,6 +17,7 @@
 #   bthreads boundary_bench at $BTHREADS host threads, with the box's cgroup CPU limits
 #   bintr    boundary_bench with the runtime's interrupt-driven waits (default) and with polling waits
 #   btrace   boundary_bench (C++ mirror ExchangeBatch) with per-phase host stamps, then under a HIP API trace
+#   tsweep   config-4 tile shapes (tools/tile_sweep.py, $TSHAPES as shape:nt_stores)
 #   xab      config-2 exchange store forms A/B (tools/exchange_ab.py)
 #   ptest    pytest -m gpu on $PTEST (a -k expression)
 #   ftime    fold timing builds tools/fold_time_$FTIME (space-separated variant names), interleaved, configs 3 and 5
@@ -76,6 +77,8 @@ for r in "$@"; do
       TAILN=30 step bplain_$TAG 200 env CRDT_TRACE_STAGE=1 go-crdt-playground_amd/host/build/boundary_bench 65536
       CRDT_TRACE_STAGE=1 TAILN=10 step btrace_$TAG 300 rocprofv3 --hip-trace --memory-copy-trace --kernel-trace --stats \
         --output-format csv -d gpurun_out/btrace_$TAG -o run -- go-crdt-playground_amd/host/build/boundary_bench 65536 ;;
+    tsweep)
+      TAILN=12 step tsweep_$TAG 400 python3 tools/tile_sweep.py 16384 ${TSHAPES:-9:1 10:1 9:1 10:1 9:1 10:1} ;;
     xab)
       TAILN=12 step xab_$TAG 400 python3 tools/exchange_ab.py ;;
     ptest)
