@@ -55,7 +55,14 @@ namespace crdt {
 //    (+3 % config 5); dropped;
 //  * tombstone check by reading a short source's <= 8 entries at once instead
 //    of binary-search probes: +8 % on config 3 (one VGPR spills); the source
-//    actors kept in a register instead of re-read from LDS: no change; dropped.
+//    actors kept in a register instead of re-read from LDS: no change; dropped;
+//  * CRDT_FOLD_NOFULL_PASS: a delta document with no full step (every step a
+//    delta) walks its slots once -- the entry/add/drop time words and the last
+//    entry row in one pass, one wave barrier fewer in the chain: config 3
+//    1.87 -> 1.81 ms (-3.7 %), config 5 unchanged, on (profiles/r04y_*);
+//  * the per-step "has a changed entry / an effective tombstone" flags OR-ed
+//    over the wave with DPP instead of written to LDS and read back: no change
+//    (within 0.3 %), kept as the simpler form.
 // 1: survivors staged through LDS and written as contiguous lines -- measured
 // 4 % slower on config 3 and 5 % on config 5 (tools/fold_probe.hip timing
 // builds, three interleaved rounds), so off: each lane stores its own
@@ -69,6 +76,9 @@ namespace crdt {
 #endif
 #ifndef CRDT_FOLD_PURE_CHUNKS
 #define CRDT_FOLD_PURE_CHUNKS 0
+#endif
+#ifndef CRDT_FOLD_NOFULL_PASS
+#define CRDT_FOLD_NOFULL_PASS 1
 #endif
 #ifndef CRDT_FOLD_LDS_PAD
 #define CRDT_FOLD_LDS_PAD 0
@@ -161,8 +171,8 @@ struct FoldSmem {
     // 8-byte aligned: the AWSet walk keeps 64-bit slot masks here, updated
     // with 64-bit LDS atomics, which fault on a misaligned address
     alignas(16) uint16_t stag[NCAP];  // kept tuples' tags
-    uint8_t anye[MCAP];              // step j has a changed entry
-    uint8_t anyt[MCAP];              // step j has an effective tombstone
+    uint8_t anye[MCAP];              // (unused since round 4: the step masks are OR-ed in registers;
+    uint8_t anyt[MCAP];              //  kept: the walks' tables reach over these bytes)
     alignas(4) uint8_t smark[NCAP];  // s + 1 where source s's entries / tombstones end (step of a tuple)
     alignas(8) uint16_t dbase[256];  // dense_sort: first sorted position of each key slot (64-bit stores)
 #if CRDT_FOLD_LDS_PAD
@@ -222,6 +232,25 @@ __device__ __forceinline__ uint32_t wave_minmax(uint32_t x) {
     x = op(x, dpp<0x142, 0xA>(id, x));  // row_bcast:15
     x = op(x, dpp<0x143, 0xC>(id, x));  // row_bcast:31
     return (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
+}
+
+// OR of a u64 over every lane (DPP scan; every lane gets the result).
+__device__ __forceinline__ uint64_t wave_or64(uint64_t v) {
+    uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
+    lo |= dpp<0x111>(0u, lo);
+    hi |= dpp<0x111>(0u, hi);
+    lo |= dpp<0x112>(0u, lo);
+    hi |= dpp<0x112>(0u, hi);
+    lo |= dpp<0x114>(0u, lo);
+    hi |= dpp<0x114>(0u, hi);
+    lo |= dpp<0x118>(0u, lo);
+    hi |= dpp<0x118>(0u, hi);
+    lo |= dpp<0x142, 0xA>(0u, lo);
+    hi |= dpp<0x142, 0xA>(0u, hi);
+    lo |= dpp<0x143, 0xC>(0u, lo);
+    hi |= dpp<0x143, 0xC>(0u, hi);
+    return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)hi, 63) << 32) |
+           (uint32_t)__builtin_amdgcn_readlane((int)lo, 63);
 }
 
 // Inclusive prefix sum over lanes (DPP).
@@ -547,6 +576,30 @@ __device__ __forceinline__ bool dense_delta_walk(Smem& m, const uint64_t (&key)[
     reinterpret_cast<uint4*>(dropw)[lane] = z4;
     wave_sync();
     uint32_t tm[4], sl[4];
+    // No full step (wave-uniform; the common case of delta anti-entropy): every
+    // kept entry adds and no gap can drop it, so the entry-time pass is not
+    // needed -- the slot's last entry is an atomic max of (time << 8 | tuple)
+    // in erows' words, in the same pass as the add and drop bits.
+    const bool nofull = CRDT_FOLD_NOFULL_PASS && full_mask == 0ull;
+    if (nofull) {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const uint32_t i = c * 64u + lane;
+            sl[c] = (uint32_t)(key[c] - kb) & 255u;
+            tm[c] = i < n ? 0u : (step[c] & 63u) * 2u + (isT[c] ? 2u : 1u);
+            if (!kept[c]) continue;
+            const uint32_t r = tm[c];
+            if (isT[c]) {
+                const uint64_t cc = m.tc[i];
+                const bool cov = a[c] < R;  // actor > R: HasDot false
+                const uint32_t j = (r - 1u) >> 1;
+                if (!(cov && m.vs[j * R + (cov ? a[c] : 0u)] >= cc)) atomicOr(&dropw[sl[c]], 1u << r);
+            } else {
+                atomicOr(&addw[sl[c]], 1u << r);
+                atomicMax(&erows[sl[c]], (r << 8) | i);
+            }
+        }
+    } else {
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
         const uint32_t i = c * 64u + lane;
@@ -583,6 +636,7 @@ __device__ __forceinline__ bool dense_delta_walk(Smem& m, const uint64_t (&key)[
         if (drop) atomicOr(&dropw[sl[c]], 1u << r);
         if (!above) last[sl[c]] = (uint8_t)i;
     }
+    }
     wave_sync();
     STAMP(9)
     // every slot's words first, then its last entry's dot (reads issued
@@ -593,7 +647,7 @@ __device__ __forceinline__ bool dense_delta_walk(Smem& m, const uint64_t (&key)[
         const uint32_t s = q * 64u + lane;
         aw[q] = addw[s];
         dw[q] = dropw[s];
-        lt8[q] = last[s];
+        lt8[q] = nofull ? (erows[s] & 0xFFu) : last[s];
     }
     uint32_t ea[4];
     uint64_t ec[4];
@@ -1016,8 +1070,6 @@ __global__ __launch_bounds__(fold_waves<DELTA>() * 64) __attribute__((amdgpu_wav
                 toffv = nto - cur.t0;
             }
             m.sact[lane] = P.act;
-            m.anye[lane] = 0;
-            m.anyt[lane] = 0;
             reinterpret_cast<uint32_t*>(m.smark)[lane & (Smem::NCAP / 4 - 1)] = 0u;
             wave_sync();
             // Source s's tuples end at soffv / toffv (nondecreasing in s): mark
@@ -1130,6 +1182,7 @@ __global__ __launch_bounds__(fold_waves<DELTA>() * 64) __attribute__((amdgpu_wav
             STAMP(11)
             uint64_t key[NCH];
             uint32_t flag = 0, perr = 0;  // flag bit c: changed entry / effective tombstone
+            uint64_t me = 0, mt = 0;      // steps of this lane's changed entries / effective tombstones
 #pragma unroll
             for (int c = 0; c < NCH; ++c) {
                 key[c] = 0;
@@ -1145,7 +1198,7 @@ __global__ __launch_bounds__(fold_waves<DELTA>() * 64) __attribute__((amdgpu_wav
                         // MakeDeltaMergeData (:84-92): dst's clock has not seen the entry
                         if (a == R) perr |= kErrActorRange;
                         f = !(a < R && m.vs[j * R + a] >= cc);
-                        if (f) m.anye[j] = 1;
+                        me |= f ? 1ull << j : 0ull;
                     }
                     if (DELTA && isT[c]) {
                         // effective: not re-added in the same source (:93-102)
@@ -1159,21 +1212,24 @@ __global__ __launch_bounds__(fold_waves<DELTA>() * 64) __attribute__((amdgpu_wav
                         }
                         const bool in_s = pos < len && m.tk[lo + pos] == key[c];
                         f = !(in_s && (m.ta[lo + pos] != a || m.tc[lo + pos] > cc));
-                        if (f) m.anyt[j] = 1;
+                        mt |= f ? 1ull << j : 0ull;
                     }
                     flag |= f ? (1u << c) : 0u;
                 }
             }
             wave_sync();
             STAMP(3)
-            uint64_t noop_mask = 0;
+            uint64_t noop_mask = 0, tmask = 0;
             if (DELTA) {
-                const bool nz = lane < ms && !((full_mask >> lane) & 1ull) && !m.anye[lane] && !m.anyt[lane];
-                noop_mask = ballot(nz);
+                // steps with a changed entry / an effective tombstone, OR-ed over the
+                // wave in registers (DPP): no LDS round trip
+                const uint64_t anye = wave_or64(me);
+                tmask = wave_or64(mt) & low_mask(ms);
+                noop_mask = low_mask(ms) & ~full_mask & ~anye & ~tmask;
             }
             if (DELTA && noop_mask) {
                 // a step brings nothing: replay the schedule step by step with the exact clocks
-                const uint64_t emask = ballot(lane < ms && m.anyt[lane]);
+                const uint64_t emask = tmask;
                 v = vreg;
                 full_mask = 0;
                 noop_mask = 0;

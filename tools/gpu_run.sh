@@ -30,7 +30,7 @@ for r in "$@"; do
   case $r in
     tests)
       TAILN=4 step gpu_tests 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread
-      grep -q " FAILED\| ERROR" gpurun_out/gpu_tests.log && { echo "tests failed"; exit 1; } ;;
+      if grep -q " FAILED\| ERROR" gpurun_out/gpu_tests.log; then echo "tests failed"; exit 1; fi ;;
     smoke)
       TAILN=2 step smoke 180 python -u -c "import __graft_entry__ as g; g.smoke()" ;;
     bench)
@@ -83,7 +83,7 @@ for r in "$@"; do
       TAILN=12 step xab_$TAG 400 python3 tools/exchange_ab.py ;;
     ptest)
       TAILN=6 step ptest_$TAG 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -k "$PTEST"
-      grep -q " FAILED\| ERROR" gpurun_out/ptest_$TAG.log && { echo "tests failed"; exit 1; } ;;
+      if grep -q " FAILED\| ERROR" gpurun_out/ptest_$TAG.log; then echo "tests failed"; exit 1; fi ;;
     *) echo "unknown recipe $r"; exit 2 ;;
   esac
 done
