@@ -62,7 +62,22 @@ namespace crdt {
 //    1.87 -> 1.81 ms (-3.7 %), config 5 unchanged, on (profiles/r04y_*);
 //  * the per-step "has a changed entry / an effective tombstone" flags OR-ed
 //    over the wave with DPP instead of written to LDS and read back: no change
-//    (within 0.3 %), kept as the simpler form.
+//    (within 0.3 %), kept as the simpler form;
+//  * tuple loads by region (one descriptor per region and array, the regions'
+//    zero-filled out-of-range loads OR-ed): +30 % on both -- three times the
+//    load instructions of a straddling chunk, plus spills; dropped.  HasDot of
+//    every source tuple computed in the classify pass (the walk then reads no
+//    clocks): +0.5 %, dropped.  8 more (out-of-range) store instructions per
+//    document: +0.7 % config 3, +7 % config 5 -- config 3 is not bound by its
+//    memory-instruction count;
+//  * CRDT_FOLD_STAGE_STORES 2 (survivors staged by slot in LDS, then 16-byte
+//    stores: 5 store instructions a document instead of 12; the range check
+//    drops each dword past the last survivor, tools/buf_probe):
+//    -1.8 % config 3, +2.5 % config 5 (profiles/r04z_fold_variants.log), off;
+//  * CRDT_FOLD_PTAB (the prefetch reads its region's base pointers from a
+//    12-entry LDS table instead of a 3-way select of scalar pointers: 330
+//    fewer static VALU in the lean delta kernel): -1.8 % config 3, +0.9 %
+//    config 5; on for the delta folds only.
 // 1: survivors staged through LDS and written as contiguous lines -- measured
 // 4 % slower on config 3 and 5 % on config 5 (tools/fold_probe.hip timing
 // builds, three interleaved rounds), so off: each lane stores its own
@@ -77,6 +92,9 @@ namespace crdt {
 #ifndef CRDT_FOLD_PURE_CHUNKS
 #define CRDT_FOLD_PURE_CHUNKS 0
 #endif
+#ifndef CRDT_FOLD_PTAB
+#define CRDT_FOLD_PTAB 1
+#endif
 #ifndef CRDT_FOLD_NOFULL_PASS
 #define CRDT_FOLD_NOFULL_PASS 1
 #endif
@@ -88,6 +106,9 @@ namespace crdt {
 #endif
 #ifndef CRDT_FOLD_PAD_SALU
 #define CRDT_FOLD_PAD_SALU 0
+#endif
+#ifndef CRDT_FOLD_PAD_VMEM
+#define CRDT_FOLD_PAD_VMEM 0
 #endif
 
 // ---- the fold restated per key ---------------------------------------------
@@ -157,7 +178,7 @@ struct FoldShape {
 };
 
 template <int VCAP_, int NCAP_>
-struct FoldSmem {
+struct alignas(16) FoldSmem {
     static constexpr int NCAP = NCAP_;  // document entries + source entries + tombstones
     static constexpr int VCAP = VCAP_;  // sources x R clock words
     static constexpr int MCAP = 64;   // sources per document
@@ -171,8 +192,8 @@ struct FoldSmem {
     // 8-byte aligned: the AWSet walk keeps 64-bit slot masks here, updated
     // with 64-bit LDS atomics, which fault on a misaligned address
     alignas(16) uint16_t stag[NCAP];  // kept tuples' tags
-    uint8_t anye[MCAP];              // (unused since round 4: the step masks are OR-ed in registers;
-    uint8_t anyt[MCAP];              //  kept: the walks' tables reach over these bytes)
+    uint8_t anye[MCAP];              // the prefetch's per-region base table (CRDT_FOLD_PTAB: 12 x 8 bytes
+    uint8_t anyt[MCAP];              //  over both; dead during a fold, whose walk tables reach over them)
     alignas(4) uint8_t smark[NCAP];  // s + 1 where source s's entries / tombstones end (step of a tuple)
     alignas(8) uint16_t dbase[256];  // dense_sort: first sorted position of each key slot (64-bit stores)
 #if CRDT_FOLD_LDS_PAD
@@ -187,6 +208,7 @@ constexpr bool fold_smem_aligned() {
     using S = FoldSmem<V, N>;
     return offsetof(S, tk) % 8 == 0 && offsetof(S, tc) % 8 == 0 && offsetof(S, vs) % 8 == 0 &&
            offsetof(S, svv) % 8 == 0 && offsetof(S, stag) % 8 == 0 && offsetof(S, dbase) % 8 == 0 &&
+           offsetof(S, anye) % 8 == 0 && offsetof(S, anyt) == offsetof(S, anye) + S::MCAP && 2 * S::MCAP >= 96 &&
            alignof(S) >= 8;
 }
 // (checked where each kernel instantiates its shape, fold_pipe_kernel)
@@ -833,7 +855,17 @@ constexpr int kFoldStoreAux = kAuxNT;
 constexpr int kFoldK = CRDT_FOLD_K;  // consecutive documents per wavefront (AWSet folds)
 constexpr int kFoldKD = CRDT_FOLD_K_DELTA;  // (delta folds: 16, measured 2 % faster than 32 on config 3)
 // stores of one document's write-out: walk rounds x 3 + count + VV
-__host__ __device__ constexpr int fold_stores(int nch) { return nch * 3 + 2; }
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+// lane E of (hi:lo) := the wave-uniform x (v_writelane: no select, no exec change)
+template <int E>
+__device__ __forceinline__ void lane_put(uint32_t& lo, uint32_t& hi, uint64_t x) {
+    asm("v_writelane_b32 %0, %1, %2" : "+v"(lo) : "s"((uint32_t)x), "i"(E));
+    asm("v_writelane_b32 %0, %1, %2" : "+v"(hi) : "s"((uint32_t)(x >> 32)), "i"(E));
+}
+// (CRDT_FOLD_STAGE_STORES 2: 16-byte stores, two keys / counters or four actors a lane)
+__host__ __device__ constexpr int fold_stores(int nch) {
+    return CRDT_FOLD_STAGE_STORES == 2 ? 2 * ((nch + 1) / 2) + (nch + 3) / 4 + 2 : nch * 3 + 2;
+}
 
 template <int K, bool DELTA, bool LEAN, bool LIST>
 __global__ __launch_bounds__(fold_waves<DELTA>() * 64) __attribute__((amdgpu_waves_per_eu(FoldShape<DELTA, LEAN>::WPE))) void fold_pipe_kernel(BatchView dst, SrcView sb, OutView out, Work wk) {
@@ -941,6 +973,48 @@ __global__ __launch_bounds__(fold_waves<DELTA>() * 64) __attribute__((amdgpu_wav
     // entries | tombstones] by per-lane address (lanes past N re-read the last
     // tuple, so no load is exec-masked), clocks and offsets by buffer loads.
     auto prefetch = [&](FoldPref<NCH, VCH>& P, const DocMeta& q) {
+        // (delta folds only: -1.8 % on config 3; the AWSet folds select between
+        // two regions, +0.9 % on config 5 -- profiles/r04z_fold_variants.log)
+        if constexpr (DELTA && CRDT_FOLD_PTAB) {
+        // Per-region base table in LDS (the 128 spare bytes at anye / anyt,
+        // dead here): entry r * 4 + {0 keys, 1 counters, 2 actors} points at
+        // tuple 0 of the document's index space in region r's array, so a lane
+        // reads its region's three bases (two LDS reads) instead of selecting
+        // among nine scalar pointers in vector registers.  Built lane by lane
+        // from scalar values (v_writelane), written by one LDS store.
+        {
+            uint64_t* ptab = reinterpret_cast<uint64_t*>(m.anye);
+            const uint64_t dn = (uint64_t)q.doff, en = (uint64_t)q.e0 - q.n, tn = (uint64_t)q.t0 - q.n - q.E;
+            uint32_t lo = 0, hi = 0;
+            lane_put<0>(lo, hi, reinterpret_cast<uint64_t>(dst.keys) + 8u * dn);
+            lane_put<1>(lo, hi, reinterpret_cast<uint64_t>(dst.counters) + 8u * dn);
+            lane_put<2>(lo, hi, reinterpret_cast<uint64_t>(dst.actors) + 4u * dn);
+            lane_put<4>(lo, hi, reinterpret_cast<uint64_t>(sb.keys) + 8u * en);
+            lane_put<5>(lo, hi, reinterpret_cast<uint64_t>(sb.counters) + 8u * en);
+            lane_put<6>(lo, hi, reinterpret_cast<uint64_t>(sb.actors) + 4u * en);
+            if (DELTA) {
+                lane_put<8>(lo, hi, reinterpret_cast<uint64_t>(sb.tkeys) + 8u * tn);
+                lane_put<9>(lo, hi, reinterpret_cast<uint64_t>(sb.tcounters) + 8u * tn);
+                lane_put<10>(lo, hi, reinterpret_cast<uint64_t>(sb.tactors) + 4u * tn);
+            }
+            if (lane < 12) ptab[lane] = ((uint64_t)hi << 32) | lo;
+            wave_sync();
+        }
+        const uint64_t* ptab = reinterpret_cast<const uint64_t*>(m.anye);
+        const uint32_t nE = q.n + q.E;
+#pragma unroll
+        for (int c = 0; c < NCH; ++c) {
+            if ((uint32_t)c * 64u < q.N) {
+                uint32_t i = c * 64u + lane;
+                i = i < q.N ? i : q.N - 1u;
+                const uint32_t r4 = (i >= q.n ? 4u : 0u) + (i >= nE ? 4u : 0u);
+                const uint64_t kb = ptab[r4], cb = ptab[r4 + 1], ab = ptab[r4 + 2];
+                P.k[c] = __builtin_nontemporal_load(reinterpret_cast<const uint64_t*>(kb) + i);
+                P.a[c] = __builtin_nontemporal_load(reinterpret_cast<const uint32_t*>(ab) + i);
+                P.c[c] = __builtin_nontemporal_load(reinterpret_cast<const uint64_t*>(cb) + i);
+            }
+        }
+        } else {
 #pragma unroll
         for (int c = 0; c < NCH; ++c) {
 #if CRDT_FOLD_PURE_CHUNKS
@@ -974,6 +1048,7 @@ __global__ __launch_bounds__(fold_waves<DELTA>() * 64) __attribute__((amdgpu_wav
                 P.a[c] = __builtin_nontemporal_load(ab + idx);
                 P.c[c] = __builtin_nontemporal_load(cb + idx);
             }
+        }
         }
         const rsrc_t rv = make_rsrc(sb.vv + (size_t)q.s0 * R, q.ms * R * 8u);
 #pragma unroll
@@ -1356,7 +1431,31 @@ __global__ __launch_bounds__(fold_waves<DELTA>() * 64) __attribute__((amdgpu_wav
             }
         }
         wave_sync();
-        {
+        if constexpr (CRDT_FOLD_STAGE_STORES == 2) {
+            // 16 bytes a lane: 128 keys / counters or 256 actors per store
+            // instruction (the descriptors end at the last survivor, and the
+            // range check drops each dword past it)
+            const rsrc_t sk = make_rsrc(out.keys + obase, min(U, capo) * 8u);
+            const rsrc_t sa = make_rsrc(out.actors + obase, min(U, capo) * 4u);
+            const rsrc_t sc = make_rsrc(out.counters + obase, min(U, capo) * 8u);
+#pragma unroll
+            for (int h = 0; h < (NCH + 1) / 2; ++h) {
+                const uint32_t i = h * 128u + 2u * lane;
+                const bool in = i < (uint32_t)Smem::NCAP;
+                const uint32_t ii = in ? i : 0u;
+                const u32x4 kv = *reinterpret_cast<const u32x4*>(&m.tk[ii]);
+                const u32x4 cv = *reinterpret_cast<const u32x4*>(&m.tc[ii]);
+                __builtin_amdgcn_raw_buffer_store_b128(kv, sk, (int)(in ? i * 8u : kOOB), 0, kFoldStoreAux);
+                __builtin_amdgcn_raw_buffer_store_b128(cv, sc, (int)(in ? i * 8u : kOOB), 0, kFoldStoreAux);
+            }
+#pragma unroll
+            for (int g = 0; g < (NCH + 3) / 4; ++g) {
+                const uint32_t i = g * 256u + 4u * lane;
+                const bool in = i < (uint32_t)Smem::NCAP;
+                const u32x4 av = *reinterpret_cast<const u32x4*>(&m.ta[in ? i : 0u]);
+                __builtin_amdgcn_raw_buffer_store_b128(av, sa, (int)(in ? i * 4u : kOOB), 0, kFoldStoreAux);
+            }
+        } else {
             const rsrc_t sk = make_rsrc(out.keys + obase, min(U, capo) * 8u);
             const rsrc_t sa = make_rsrc(out.actors + obase, min(U, capo) * 4u);
             const rsrc_t sc = make_rsrc(out.counters + obase, min(U, capo) * 8u);
@@ -1377,6 +1476,10 @@ __global__ __launch_bounds__(fold_waves<DELTA>() * 64) __attribute__((amdgpu_wav
             st32<kFoldStoreAux>(em.a[q], oa, o4);
             st64<kFoldStoreAux>(em.c[q], oc, o8);
         }
+#endif
+#if CRDT_FOLD_PAD_VMEM  // diagnostic: N more (all out-of-range) store instructions per document
+#pragma unroll
+        for (int i = 0; i < CRDT_FOLD_PAD_VMEM; ++i) st64<kFoldStoreAux>(em.k[0], ok, kOOB + 8u * i);
 #endif
         const uint32_t carry = U;
         const bool none = cur.big || deferred;
