@@ -92,6 +92,12 @@ namespace crdt {
 #ifndef CRDT_FOLD_PURE_CHUNKS
 #define CRDT_FOLD_PURE_CHUNKS 0
 #endif
+#ifndef CRDT_FOLD_AWSET_ONE_ROUND
+#define CRDT_FOLD_AWSET_ONE_ROUND 1
+#endif
+#ifndef CRDT_FOLD_CLASSIFY_UNIFORM
+#define CRDT_FOLD_CLASSIFY_UNIFORM 0
+#endif
 #ifndef CRDT_FOLD_PTAB
 #define CRDT_FOLD_PTAB 1
 #endif
@@ -212,6 +218,17 @@ constexpr bool fold_smem_aligned() {
            alignof(S) >= 8;
 }
 // (checked where each kernel instantiates its shape, fold_pipe_kernel)
+
+// A value every lane must load: consumed by an empty asm, so the compiler
+// cannot sink its (LDS) load into an exec-masked block of the lanes that use it.
+__device__ __forceinline__ uint64_t issued(uint64_t v) {
+    asm volatile("" : "+v"(v));
+    return v;
+}
+__device__ __forceinline__ uint32_t issued(uint32_t v) {
+    asm volatile("" : "+v"(v));
+    return v;
+}
 
 // Tuple tag: bits 15..8 = 0 for a document entry, (j+1)*2 for an entry of
 // source j, (j+1)*2+1 for its tombstone; bits 7..0 = tuple index in LDS.  The
@@ -575,7 +592,7 @@ __device__ __forceinline__ bool dense_delta_walk(Smem& m, const uint64_t (&key)[
         const uint32_t j = step[c] & 63u;
         const bool fj = (full_mask >> j) & 1ull, nj = (noop_mask >> j) & 1ull, f = (flag >> c) & 1u;
         kept[c] = i < N && ((i < n) || (isE[c] && !nj && (fj || f)) || (isT[c] && !nj && !fj && f));
-        a[c] = m.ta[i < N ? i : 0u];
+        a[c] = issued(m.ta[i < N ? i : 0u]);  // every lane: no exec region around the load
         anyR |= kept[c] && a[c] == R;
         const uint64_t d = key[c] - b + 0x80000000ull;
         bad |= kept[c] && (d >> 32) != 0;
@@ -872,6 +889,11 @@ __global__ __launch_bounds__(fold_waves<DELTA>() * 64) __attribute__((amdgpu_wav
     static_assert(!(LEAN && LIST), "the lean pass runs over consecutive documents");
     static_assert(K >= 1 && K < 64, "a run's end bounds live in lane K: K < 64");
     constexpr int NCH = FoldShape<DELTA, LEAN>::NCH, VCH = FoldShape<DELTA, LEAN>::VCH;
+    // store rounds of a write-out: the lean AWSet pass emits only through
+    // dense_awset_walk (slots < 64: one round; a document it cannot walk is
+    // deferred, nothing written), so its second round would be all out of
+    // range -- not issued (config 5: 3 fewer store instructions a document)
+    constexpr int WQ = (LEAN && !DELTA && CRDT_FOLD_AWSET_ONE_ROUND) ? 1 : NCH;
     using Smem = FoldSmem<FoldShape<DELTA, LEAN>::VCAP, 64 * NCH>;
     static_assert(fold_smem_aligned<FoldShape<DELTA, LEAN>::VCAP, 64 * NCH>(),
                   "FoldSmem: a 64-bit LDS access target is not 8-byte aligned");
@@ -1077,7 +1099,7 @@ __global__ __launch_bounds__(fold_waves<DELTA>() * 64) __attribute__((amdgpu_wav
         // for the staged registers is then exact on both paths into the loop.
         const rsrc_t none = make_rsrc(out.counts, 0u);
 #pragma unroll
-        for (int i = 0; i < fold_stores(NCH); ++i) st32(0u, none, kOOB + 4u * i);  // distinct: not merged
+        for (int i = 0; i < fold_stores(WQ); ++i) st32(0u, none, kOOB + 4u * i);  // distinct: not merged
     }
 #pragma unroll 1
     for (uint32_t k = 0; k < cnt; ++k) {
@@ -1269,6 +1291,41 @@ __global__ __launch_bounds__(fold_waves<DELTA>() * 64) __attribute__((amdgpu_wav
                     const uint64_t cc = m.tc[ii];
                     const uint32_t j = step[c] & 63u;
                     bool f = false;
+#if CRDT_FOLD_CLASSIFY_UNIFORM
+                    // Wave-uniform guards (does the chunk hold entries / tombstones)
+                    // and predicated per-lane work: no exec-mask regions per chunk.
+                    const uint32_t c64 = c * 64u;
+                    if (DELTA && c64 < n + E && c64 + 64u > n) {
+                        // MakeDeltaMergeData (:84-92): dst's clock has not seen the entry
+                        const bool ce = isE[c] && !((full_mask >> j) & 1ull);
+                        perr |= (ce && a == R) ? kErrActorRange : 0u;
+                        const bool cov = a < R;
+                        const uint64_t vj = issued(m.vs[j * R + (cov ? a : 0u)]);
+                        const bool fe = ce && !(cov && vj >= cc);
+                        me |= fe ? 1ull << j : 0ull;
+                        f = fe;
+                    }
+                    if (DELTA && c64 + 64u > n + E && c64 < N) {
+                        // effective: not re-added in the same source (:93-102); lanes
+                        // that are not tombstones search an empty range
+                        const uint32_t s0 = m.soff[j], lo = n + s0, len = isT[c] ? m.soff[j + 1] - s0 : 0u;
+                        uint32_t pos = 0;
+                        for (uint32_t st = 256; st > 0; st >>= 1) {
+                            if (st > cmax) continue;
+                            const bool in = pos + st <= len;
+                            const uint64_t v2 = issued(m.tk[in ? lo + pos + st - 1 : 0u]);
+                            pos += (in && v2 < key[c]) ? st : 0u;
+                        }
+                        const bool hit = pos < len;
+                        const uint32_t at = hit ? lo + pos : 0u;
+                        const uint64_t hk = issued(m.tk[at]), hc = issued(m.tc[at]);
+                        const uint32_t ha = issued(m.ta[at]);
+                        const bool in_s = hit && hk == key[c];
+                        const bool ft = isT[c] && !(in_s && (ha != a || hc > cc));
+                        mt |= ft ? 1ull << j : 0ull;
+                        f = f || ft;
+                    }
+#else
                     if (DELTA && isE[c] && !((full_mask >> j) & 1ull)) {
                         // MakeDeltaMergeData (:84-92): dst's clock has not seen the entry
                         if (a == R) perr |= kErrActorRange;
@@ -1289,6 +1346,7 @@ __global__ __launch_bounds__(fold_waves<DELTA>() * 64) __attribute__((amdgpu_wav
                         f = !(in_s && (m.ta[lo + pos] != a || m.tc[lo + pos] > cc));
                         mt |= f ? 1ull << j : 0ull;
                     }
+#endif
                     flag |= f ? (1u << c) : 0u;
                 }
             }
@@ -1469,7 +1527,7 @@ __global__ __launch_bounds__(fold_waves<DELTA>() * 64) __attribute__((amdgpu_wav
         }
 #else
 #pragma unroll
-        for (int q = 0; q < NCH; ++q) {
+        for (int q = 0; q < WQ; ++q) {
             const uint32_t o = em.off[q];
             const uint32_t o8 = o == kOOB ? kOOB : o * 8u, o4 = o == kOOB ? kOOB : o * 4u;
             st64<kFoldStoreAux>(em.k[q], ok, o8);
