@@ -237,8 +237,16 @@ __device__ __forceinline__ void join_doc(JoinWaveSmem<WAVES>& sm, uint32_t w, co
 // ping-pong pipeline -- the next document's entries are issued before this
 // one is merged.  The body is straight-line buffer VMEM, so the compiler's
 // vmcnt waits count exactly and the prefetch stays in flight.
+#ifndef CRDT_JOIN_WPE  // waves per SIMD the compiler must fit (0: its own choice -- 106 SGPRs, 7 waves)
+#define CRDT_JOIN_WPE 0
+#endif
+#if CRDT_JOIN_WPE
+#define CRDT_JOIN_WPE_ATTR __attribute__((amdgpu_waves_per_eu(CRDT_JOIN_WPE)))
+#else
+#define CRDT_JOIN_WPE_ATTR
+#endif
 template <int WAVES, int K, int AUX, bool EXCH, bool STG>
-__global__ __launch_bounds__(WAVES * 64) void join_wave_kernel(BatchView dst, BatchView src, OutView out, OutView out2,
+__global__ __launch_bounds__(WAVES * 64) CRDT_JOIN_WPE_ATTR void join_wave_kernel(BatchView dst, BatchView src, OutView out, OutView out2,
                                                                Work wk, uint32_t no_large, SlabMap slabs) {
     __shared__ JoinWaveSmem<WAVES> sm;
     const uint32_t lane = threadIdx.x & 63;

@@ -20,6 +20,7 @@
 #   tsweep   config-4 tile shapes (tools/tile_sweep.py, $TSHAPES as shape:nt_stores)
 #   xab      config-2 exchange store forms A/B (tools/exchange_ab.py)
 #   ptest    pytest -m gpu on $PTEST (a -k expression)
+#   jab      config-2 exchange timed per library build ($JLIBS: base = the product library, X = tools/libcrdtgpu_X.so)
 #   ftime    fold timing builds tools/fold_time_$FTIME (space-separated variant names), interleaved, configs 3 and 5
 set -u
 cd "$(dirname "$0")/.."
@@ -52,6 +53,11 @@ for r in "$@"; do
       TAILN=20 step probe_c5 120 tools/fold_probe 5 ;;
     multi)
       TAILN=4 step multirank 300 python -u -m pytest tests/test_gpu_multirank.py -x -v --timeout 240 --timeout-method thread ;;
+    jab)
+      for r in 1 2 3; do for v in ${JLIBS:-base}; do
+        lib=go-crdt-playground_amd/crdtgpu/libcrdtgpu.so; [ "$v" = base ] || lib=tools/libcrdtgpu_$v.so
+        TAILN=1 step jab_${v}_$r 180 env CRDTGPU_LIB=$PWD/$lib python3 tools/exchange_time.py
+      done; done ;;
     ftime)
       for r in 1 2 3; do for v in ${FTIME:-base}; do for c in 3 5; do
         TAILN=1 step ftime_${v}_c${c}_$r 120 tools/fold_time_$v $c
