@@ -77,7 +77,15 @@ namespace crdt {
 //  * CRDT_FOLD_PTAB (the prefetch reads its region's base pointers from a
 //    12-entry LDS table instead of a 3-way select of scalar pointers: 330
 //    fewer static VALU in the lean delta kernel): -1.8 % config 3, +0.9 %
-//    config 5; on for the delta folds only.
+//    config 5; on for the delta folds only;
+//  * CRDT_FOLD_IDX32 (the AWSet prefetch selects 32-bit slot indices and knows
+//    it has no tombstone region: no exec-masked 64-bit arithmetic; -74 static
+//    VALU, -33 SALU): config 5 -3 % (noisy), on;
+//  * CRDT_FOLD_CLASSIFY_UNIFORM (chunk-uniform guards + predicated per-lane
+//    entry / tombstone checks in the delta classify, -80 static SALU): +1.3 %
+//    on config 3, off.  PMC of the lean delta pass at HEAD: 691 VALU, 485 SALU,
+//    97 LDS instructions a document (round 3: 837 / 533 / 104;
+//    profiles/r04c3_pmc_summary.txt).
 // 1: survivors staged through LDS and written as contiguous lines -- measured
 // 4 % slower on config 3 and 5 % on config 5 (tools/fold_probe.hip timing
 // builds, three interleaved rounds), so off: each lane stores its own
@@ -97,6 +105,9 @@ namespace crdt {
 #endif
 #ifndef CRDT_FOLD_CLASSIFY_UNIFORM
 #define CRDT_FOLD_CLASSIFY_UNIFORM 0
+#endif
+#ifndef CRDT_FOLD_IDX32
+#define CRDT_FOLD_IDX32 1
 #endif
 #ifndef CRDT_FOLD_PTAB
 #define CRDT_FOLD_PTAB 1
@@ -1059,9 +1070,16 @@ __global__ __launch_bounds__(fold_waves<DELTA>() * 64) __attribute__((amdgpu_wav
             if ((uint32_t)c * 64u < q.N) {
                 uint32_t i = c * 64u + lane;
                 i = i < q.N ? i : q.N - 1u;
+#if CRDT_FOLD_IDX32
+                // 32-bit index selects (slot indices are u32), no tombstone region
+                // in an AWSet fold: no exec-masked 64-bit arithmetic per region
+                const bool isd = i < q.n, iss = !DELTA || i < q.n + q.E;
+                const size_t idx = isd ? q.doff + i : (iss ? q.e0 + (i - q.n) : q.t0 + (i - q.n - q.E));
+#else
                 const bool isd = i < q.n, iss = i < q.n + q.E;
                 const size_t idx = isd ? (size_t)q.doff + i
                                        : (iss ? (size_t)q.e0 + (i - q.n) : (size_t)q.t0 + (i - q.n - q.E));
+#endif
                 const uint64_t* kb = isd ? dst.keys : (iss ? sb.keys : sb.tkeys);
                 const uint32_t* ab = isd ? dst.actors : (iss ? sb.actors : sb.tactors);
                 const uint64_t* cb = isd ? dst.counters : (iss ? sb.counters : sb.tcounters);
