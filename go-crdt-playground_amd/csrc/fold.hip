@@ -85,7 +85,9 @@ namespace crdt {
 //    entry / tombstone checks in the delta classify, -80 static SALU): +1.3 %
 //    on config 3, off.  PMC of the lean delta pass at HEAD: 691 VALU, 485 SALU,
 //    97 LDS instructions a document (round 3: 837 / 533 / 104;
-//    profiles/r04c3_pmc_summary.txt).
+//    profiles/r04c3_pmc_summary.txt);
+//  * documents per wave (CRDT_FOLD_K_DELTA / CRDT_FOLD_K) 8 / 16 and 24 / 48
+//    against 16 / 32: equal or slower on both configs, 16 / 32 kept.
 // 1: survivors staged through LDS and written as contiguous lines -- measured
 // 4 % slower on config 3 and 5 % on config 5 (tools/fold_probe.hip timing
 // builds, three interleaved rounds), so off: each lane stores its own
