@@ -8,8 +8,9 @@ state, R = 2, synthetic reachable states generated on the device
 document the two merges A <- B and B <- A of one snapshot (one exchange launch,
 crdt_awset_exchange_async), then the per-GPU causal-context summary
 (elementwise max of the output VVs), all-reduced (max, u64) across GPUs over
-RCCL when N > 1 -- on the engine's own communicator, through the C ABI
-(crdt_comm_init + crdt_context_allreduce_async), not torch's.
+RCCL when N > 1 (torch.distributed's nccl backend; --engine-comm: the
+engine's own communicator through the C ABI, crdt_comm_init +
+crdt_context_allreduce_async, the form a Go caller binds).
 
 The same JSON line carries one "legs" entry per other BASELINE config, each
 timed the same way (warmup, barrier + synchronize, K steps, max over ranks),
@@ -79,8 +80,63 @@ def box_probe(eng, dev, nbytes=2 << 30, reps=10):
     def best(prefix):
         return max(v for k, v in variants.items() if k.startswith(prefix))
 
+    ident = box_identity(dev)  # right after the probes: the clock levels under load, if the driver shows them
     return {"bytes": nbytes, "reps": reps, "read_gbs": best("read"), "write_gbs": best("write"),
-            "copy_gbs": best("copy"), "mix_gbs": best("mix"), "sclk_mhz": eng.clock_probe(), "variants": variants}
+            "copy_gbs": best("copy"), "mix_gbs": best("mix"), "sclk_mhz": eng.clock_probe(), "variants": variants,
+            "identity": ident}
+
+
+def _sysfs_card(pci):
+    """The /sys/class/drm card directory of the PCI function `pci` (e.g. 0000:75:00.0), or None."""
+    import glob
+
+    for d in sorted(glob.glob("/sys/class/drm/card*/device")):
+        try:
+            if os.path.basename(os.path.realpath(d)).lower() == pci.lower():
+                return d
+        except OSError:
+            continue
+    return None
+
+
+def _read(path):
+    try:
+        with open(path) as f:
+            return f.read().strip()
+    except OSError:
+        return None
+
+
+def box_identity(dev):
+    """What the bandwidth probes alone do not say about this box (the
+    same exchange kernel ran 0.99 ms on one box and 1.23 ms on another): the
+    GPU's PCI function, its compute units and XCDs as the process sees them,
+    the compute / memory partition modes, and the memory (mclk), fabric (fclk)
+    and shader (sclk) clock levels the driver exposes, the active level marked
+    '*'.  sysfs, read-only; fields the box does not expose are null."""
+    import torch
+
+    p = torch.cuda.get_device_properties(dev)
+    pci = "%04x:%02x:%02x.0" % (getattr(p, "pci_domain_id", 0), getattr(p, "pci_bus_id", 0),
+                                getattr(p, "pci_device_id", 0))
+    cus = int(p.multi_processor_count)
+    out = {"pci": pci, "name": p.name, "gcn_arch": getattr(p, "gcnArchName", None), "cus": cus,
+           "xcds": cus // 32 if cus % 32 == 0 else None, "l2_bytes": getattr(p, "L2_cache_size", None),
+           "total_mem_bytes": int(p.total_memory)}
+    d = _sysfs_card(pci)
+    out["sysfs"] = d
+    if d:
+        for f in ("current_compute_partition", "current_memory_partition", "available_compute_partition",
+                  "available_memory_partition"):
+            out[f] = _read(os.path.join(d, f))
+        for f in ("pp_dpm_mclk", "pp_dpm_fclk", "pp_dpm_sclk", "pp_dpm_socclk"):
+            v = _read(os.path.join(d, f))
+            out[f] = v.splitlines() if v else None
+            act = [x for x in (out[f] or []) if x.endswith("*")]
+            out[f + "_active"] = act[0] if act else None
+        out["power_dpm_force_performance_level"] = _read(os.path.join(d, "power_dpm_force_performance_level"))
+        out["mem_info_vram_used"] = _read(os.path.join(d, "mem_info_vram_used"))
+    return out
 
 
 def _np_copy(t, n, dt):
@@ -161,6 +217,7 @@ class Config2:
     R = 2
     name = "config2"
     kernel = "join_wave_kernel"
+    tus = ("join.hip",)  # translation units of the timed kernels (crdtgpu.srcid)
     metric = "replica-merges/sec (AWSet full-state join) + achieved HBM GB/s (% roofline)"
     exchange = True  # both merges from one read (crdt_awset_exchange_async); --separate: two join launches
     shared_keys = True  # the two outputs share one key column (same keys, same slots); --own-keys: one each
@@ -184,6 +241,12 @@ class Config2:
         self.ctx_ba = torch.zeros(R, dtype=torch.int64, device=dev)
         self.a, self.b = self.A.as_batch(), self.B.as_batch()
         self.merges_per_step = 2 * n
+
+    @property
+    def kernel_instance(self):
+        """The exact template instance the timed call launches (the ABI's default
+        options: 8 docs per wave, non-temporal stores, staged stores)."""
+        return "join_wave_kernel<4, 8, 2, %s, true>" % ("true" if self.exchange else "false")
 
     def _key_owner(self):
         """B <- A uses A <- B's key column when the exchange shares one."""
@@ -269,6 +332,7 @@ class Config4(Config2):
     R = 2
     name = "config4"
     kernel = "join_tile_pipe_kernel"
+    tus = ("join.hip", "tile.hip")
     # the tile kernel is latency-bound: one shared key column saves 0.3 % of its
     # time (9.84 vs 9.87 ms), so this leg keeps a key column per output
     shared_keys = False
@@ -301,6 +365,10 @@ class Config4(Config2):
         self.a, self.b = self.A.as_batch(), self.B.as_batch()
         self.merges_per_step = 2 * n
         self.sizes = sizes
+
+    @property
+    def kernel_instance(self):
+        return "join_tile_pipe_kernel<512, 2, %s, true, true>" % ("true" if self.exchange else "false")
 
     @property
     def kernel_name(self):
@@ -339,6 +407,8 @@ class Config3:
     M = 10
     name = "config3"
     kernel = "fold_pipe_kernel"
+    kernel_instance = "fold_pipe_kernel<16, true, true, false>"
+    tus = ("fold.hip",)
     kernel_name = ("fold_pipe_kernel<16, true, true, false> (per-document fold, delta: lean slot-walk pass, then the "
                    "general pass over the documents it defers; timed as the whole call)")
     metric = "replica-merges/sec (AWSetDelta fold, config 3) + achieved HBM GB/s (% roofline)"
@@ -415,6 +485,7 @@ class Config5(Config3):
     E = 16
     name = "config5"
     kernel = "fold_pipe_kernel"
+    kernel_instance = "fold_pipe_kernel<32, false, true, false>"
     kernel_name = ("fold_pipe_kernel<32, false, true, false> (per-document fold, awset: lean slot-walk pass, then the "
                    "general pass over the documents it defers; timed as the whole call)")
     metric = "replica-merges/sec (AWSet fold r0<-..<-r7, config 5) + achieved HBM GB/s (% roofline)"
@@ -474,19 +545,35 @@ DEFAULT_DOCS = {2: 1 << 20, 3: 1 << 20, 4: 16_384, 5: 12_500_000}
 
 def _traffic(path, config, n, W):
     """HBM bytes per launch of this kernel from the PMC passes (tools/pmc.sh ->
-    tools/traffic.py --emit), matched on config, docs and kernel instance."""
+    tools/traffic.py --emit), or None.  An entry counts only when it was taken
+    on exactly what is timed: the same config, docs, exchange form and key
+    sharing, the exact kernel instance (W.kernel_instance) and the same source
+    id (crdtgpu.srcid over the kernel's translation units, W.tus).  Returns
+    (bytes or None, note, entry)."""
+    from crdtgpu.srcid import source_id
+
+    want_id = source_id(W.tus)
+    exch = bool(getattr(W, "exchange", False))
+    inst = W.kernel_instance
     if not os.path.exists(path):
-        return None
+        return None, "no %s" % os.path.basename(path), None
     try:
-        for e in json.load(open(path)):
-            exch = bool(getattr(W, "exchange", False))
-            if (e.get("docs") == n and e.get("config") == config and e.get("kernel", "").startswith(W.kernel)
-                    and bool(e.get("exchange")) == exch
-                    and (not exch or bool(e.get("shared_keys", False)) == bool(W.shared_keys))):
-                return e.get("hbm_bytes_per_launch")
-    except Exception:
-        return None
-    return None
+        table = json.load(open(path))
+    except Exception as e:
+        return None, "%s unreadable: %s" % (os.path.basename(path), e), None
+    stale = None
+    for e in table:
+        if (e.get("docs") == n and e.get("config") == config and e.get("kernel") == inst
+                and bool(e.get("exchange")) == exch
+                and (not exch or bool(e.get("shared_keys", False)) == bool(W.shared_keys))):
+            if e.get("src_id") == want_id:
+                return e.get("hbm_bytes_per_launch"), "PMC of %s at source id %s (%s)" % (
+                    inst, want_id, e.get("profile", "?")), e
+            stale = e
+    if stale is not None:
+        return None, "the PMC entry for %s was taken at source id %s, the library is at %s: not reported" % (
+            inst, stale.get("src_id"), want_id), None
+    return None, "no PMC entry for %s (config %d, %d docs)" % (inst, config, n), None
 
 
 def _box_fields(roof, box):
@@ -501,6 +588,10 @@ def _box_fields(roof, box):
         roof["box_mix_gbs"] = box.get("mix_gbs")
         roof["frac_vs_box_mix"] = a / box["mix_gbs"] if box.get("mix_gbs") else None
         roof["box_sclk_mhz"] = box.get("sclk_mhz")
+        ident = box.get("identity") or {}
+        roof["box_mclk"] = ident.get("pp_dpm_mclk_active")
+        roof["box_partition"] = "%s/%s" % (ident.get("current_compute_partition"), ident.get("current_memory_partition"))
+        roof["box_xcds"] = ident.get("xcds")
 
 
 def run_config(config, n, args, ctx, steps, warmup, repeats, cpu, box=None):
@@ -511,7 +602,7 @@ def run_config(config, n, args, ctx, steps, warmup, repeats, cpu, box=None):
 
     from crdtgpu.dist import u64_max_allreduce
 
-    eng, dev, stream, dist, world, rank = ctx
+    eng, dev, stream, dist, world, rank, engine_comm = ctx
     backend_is_host = dist is not None and dist.get_backend() != "nccl"
     seed = args.seed + (rank << 40)  # each rank owns its own documents (weak scaling)
     cls = CONFIGS[config]
@@ -568,8 +659,11 @@ def run_config(config, n, args, ctx, steps, warmup, repeats, cpu, box=None):
         if dist is not None:
             if backend_is_host:  # gloo rehearsal: torch.distributed on host copies
                 return u64_max_allreduce(dist, local_ctx.cpu()).to(dev)
-            # the engine's own RCCL communicator, through the C ABI a Go caller binds
-            eng.context_allreduce_async(local_ctx, W.R, stream=stream)
+            if engine_comm:
+                # the engine's own RCCL communicator, through the C ABI a Go caller binds
+                eng.context_allreduce_async(local_ctx, W.R, stream=stream)
+            else:  # torch.distributed over RCCL (nccl backend), u64 max via the sign flip
+                return u64_max_allreduce(dist, local_ctx)
         return local_ctx
 
     if graph is None:
@@ -605,7 +699,7 @@ def run_config(config, n, args, ctx, steps, warmup, repeats, cpu, box=None):
     extra = [timed()[:2] for _ in range(max(0, repeats - 1))]
     eng.sync(stream)
     achieved = bytes_launch / t_launch / 1e9
-    traffic = _traffic(args.traffic_json, config, n, W)
+    traffic, traffic_note, _ = _traffic(args.traffic_json, config, n, W)
     merges = W.merges_per_step * world * steps
     res = {
         "metric": W.metric,
@@ -618,7 +712,8 @@ def run_config(config, n, args, ctx, steps, warmup, repeats, cpu, box=None):
         "config": W.describe(world),
         "roofline": {
             "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": getattr(W, "kernel_name", W.kernel),
+            "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_note,
+            "kernel": getattr(W, "kernel_name", W.kernel), "kernel_instance": W.kernel_instance,
             "algorithmic_bytes_per_launch": bytes_launch, "launch_ms": t_launch * 1e3,
         },
         "replay_check": replay_check,
@@ -744,6 +839,9 @@ def main():
     ap.add_argument("--no-box-probe", action="store_true", help="skip the box bandwidth probes")
     ap.add_argument("--no-sort", action="store_true", help="skip the ingest-sort leg")
     ap.add_argument("--boundary-docs", type=int, default=65536)
+    ap.add_argument("--engine-comm", action="store_true",
+                    help="N > 1: all-reduce the summary on the engine's own RCCL communicator through the C ABI "
+                         "(crdt_comm_init + crdt_context_allreduce_async) instead of torch.distributed's")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
     args = ap.parse_args()
 
@@ -773,19 +871,26 @@ def main():
     stream = torch.cuda.current_stream()
     eng = crdtgpu.Engine(gpu)
     collective = None
+    engine_comm = False
     if world > 1:
-        if backend == "nccl":
+        if backend == "nccl" and args.engine_comm:
             # crdt_comm_unique_id on rank 0, the id shared once over torch.distributed,
             # crdt_comm_init on every rank: the per-step summary all-reduce is then
-            # crdt_context_allreduce_async (RCCL, u64 max) on the engine's communicator
+            # crdt_context_allreduce_async (RCCL, u64 max) on the engine's communicator.
+            # Opt-in: this form has run at one rank only (the pool's boxes have one GPU;
+            # tests/test_gpu_comm.py::test_engine_comm_two_ranks runs it when >= 2 are visible).
             from crdtgpu.dist import engine_comm_handshake
 
             engine_comm_handshake(dist, world, rank, eng.comm_init)
+            engine_comm = True
             collective = ("crdt_context_allreduce_async: RCCL all-reduce(max, u64) of R words on the engine's own "
                           "communicator (crdt_comm_unique_id + crdt_comm_init), once per step")
+        elif backend == "nccl":
+            collective = ("torch.distributed all-reduce(MAX) over RCCL (nccl backend) of the R-word summary, u64 order "
+                          "by a sign-bit flip (crdtgpu/dist.py u64_max_allreduce), once per step")
         else:
             collective = "torch.distributed %s all-reduce of host copies (rehearsal)" % backend
-    ctx = (eng, dev, stream, dist, world, rank)
+    ctx = (eng, dev, stream, dist, world, rank, engine_comm)
 
     if args.legs is None:
         legs = [3, 4, 5] if args.config == 2 else []

@@ -124,8 +124,18 @@ def _load():
     rts = hip_runtimes_mapped()
     if len(rts) > 1:
         raise ImportError("two HIP runtimes mapped into one process: %s" % rts)
+    for name, (res, args) in signatures().items():
+        f = getattr(lib, name)
+        f.restype = res
+        f.argtypes = args
+    return lib
+
+
+def signatures():
+    """name -> (restype, argtypes) of every entry point the package binds
+    (include/crdtgpu.h; tests/test_abi.py checks the argument counts)."""
     P = ctypes.POINTER
-    sig = {
+    return {
         "crdt_abi_version": (ctypes.c_int, []),
         "crdt_strerror": (ctypes.c_char_p, [ctypes.c_int]),
         "crdt_ctx_create": (ctypes.c_int, [ctypes.c_int, P(_vp)]),
@@ -174,11 +184,6 @@ def _load():
         "crdt_comm_init": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, _vp]),
         "crdt_context_allreduce_async": (ctypes.c_int, [_vp, _vp, _u32, _vp]),
     }
-    for name, (res, args) in sig.items():
-        f = getattr(lib, name)
-        f.restype = res
-        f.argtypes = args
-    return lib
 
 
 _lib = None

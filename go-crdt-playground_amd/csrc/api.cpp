@@ -466,10 +466,32 @@ int crdt_awset_join_async(crdt_ctx* ctx, const crdt_awset_batch* dst, const crdt
 int crdt_awset_exchange_async(crdt_ctx* ctx, const crdt_awset_batch* a, const crdt_awset_batch* b,
                               const crdt_awset_out* out_ab, const crdt_awset_out* out_ba, void* stream) {
     // out_ba->keys == out_ab->keys: one shared key column (both directions hold
-    // the same keys at the same slots); every other array must be its own
-    if (!out_ab || !out_ba || out_ab->actors == out_ba->actors || out_ab->counters == out_ba->counters ||
-        out_ab->vv == out_ba->vv || out_ab->counts == out_ba->counts)
-        return CRDT_E_INVALID;
+    // the same keys at the same slots); every other array must be its own.
+    // Checked here: no two of the twelve arrays start at the same address
+    // (keys == keys excepted), and the per-document arrays, whose sizes the
+    // host knows (offsets, counts, vv), do not overlap at all.  The entry
+    // arrays' capacity lives in device memory, so a partial overlap of them
+    // cannot be checked and is undefined (include/crdtgpu.h).
+    if (!out_ab || !out_ba || !a) return CRDT_E_INVALID;
+    const size_t n = a->n_docs, R = a->R;
+    struct Range {
+        uintptr_t p;
+        size_t bytes;  // 0: size unknown here (entry arrays)
+    };
+    const Range r[12] = {{(uintptr_t)out_ab->offsets, (n + 1) * 4}, {(uintptr_t)out_ab->counts, n * 4},
+                         {(uintptr_t)out_ab->vv, n * R * 8},       {(uintptr_t)out_ab->keys, 0},
+                         {(uintptr_t)out_ab->actors, 0},           {(uintptr_t)out_ab->counters, 0},
+                         {(uintptr_t)out_ba->offsets, (n + 1) * 4}, {(uintptr_t)out_ba->counts, n * 4},
+                         {(uintptr_t)out_ba->vv, n * R * 8},       {(uintptr_t)out_ba->keys, 0},
+                         {(uintptr_t)out_ba->actors, 0},           {(uintptr_t)out_ba->counters, 0}};
+    for (int i = 0; i < 12; ++i)
+        for (int j = i + 1; j < 12; ++j) {
+            if (i == 3 && j == 9) continue;  // the shared key column
+            if (!r[i].p || !r[j].p) continue;  // NULL pointers are rejected by join_common
+            if (r[i].p == r[j].p) return CRDT_E_INVALID;
+            if (r[i].bytes && r[j].bytes && r[i].p < r[j].p + r[j].bytes && r[j].p < r[i].p + r[i].bytes)
+                return CRDT_E_INVALID;
+        }
     return join_common(ctx, a, b, out_ab, out_ba, stream);
 }
 

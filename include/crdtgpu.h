@@ -187,7 +187,10 @@ int crdt_awset_join_async(crdt_ctx* ctx, const crdt_awset_batch* dst, const crdt
  * states.  Both directions keep the same keys at the same slots; only a
  * common key's dot differs (the src dot wins, awset.go:142).  So the two
  * outputs may share one key column: out_ba->keys == out_ab->keys is allowed
- * and writes the keys once; every other output array must be distinct.
+ * and writes the keys once; every other output array must be distinct and
+ * must not overlap another (CRDT_E_INVALID when two arrays start at the same
+ * address or the per-document arrays overlap; a partial overlap of the entry
+ * arrays, whose capacity is in device memory, is undefined behaviour).
  * (crdt_awset_exchange_batch: the same for host outputs -- the shared column
  * is also downloaded once.) */
 int crdt_awset_exchange_async(crdt_ctx* ctx, const crdt_awset_batch* a, const crdt_awset_batch* b,

@@ -21,6 +21,7 @@ _FIRST = (
     "test_gpu_parity.py::test_exchange_config2_full_size",
     "test_gpu_parity.py::test_config3_full_size",
     "test_gpu_parity.py::test_gen_replicas_and_config5_fold",
+    "test_gpu_parity.py::test_config5_bench_size",
     "test_gpu_tiles.py::test_config4_full_size_exchange",
     "test_gpu_parity.py::test_config4_zipf_slice_exact",
 )

@@ -134,3 +134,99 @@ def test_go_binding_calls_declared_entry_points():
         assert must in used
     code = re.sub(r'//[^\n]*|"(?:[^"\\]|\\.)*"', "", go)  # comments and string literals out
     assert code.count("{") == code.count("}") and code.count("(") == code.count(")")
+
+
+def _header_api():
+    """include/crdtgpu.h -> ({function: n_params}, {struct typedef: [field names]})."""
+    import re
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    hdr = open(os.path.join(root, "include", "crdtgpu.h")).read()
+    hdr = re.sub(r"/\*.*?\*/", "", hdr, flags=re.S)
+    hdr = re.sub(r"//[^\n]*", "", hdr)
+    funcs = {}
+    for m in re.finditer(r"\b(crdt_\w+)\s*\(([^;{]*?)\)\s*;", hdr, flags=re.S):
+        params = m.group(2).strip()
+        funcs[m.group(1)] = 0 if params in ("", "void") else params.count(",") + 1
+    structs = {}
+    for m in re.finditer(r"typedef\s+struct\s*\{(.*?)\}\s*(crdt_\w+)\s*;", hdr, flags=re.S):
+        structs[m.group(2)] = re.findall(r"(\w+)\s*(?:\[[^\]]*\])?\s*;", m.group(1))
+    return funcs, structs
+
+
+def _go_calls(code):
+    """(name, n_args) of every C.crdt_*(...) call in Go source (comments/strings removed)."""
+    import re
+
+    out = []
+    for m in re.finditer(r"\bC\.(crdt_\w+)\(", code):
+        i, depth, args, cur = m.end(), 1, 0, ""
+        while depth:
+            ch = code[i]
+            if ch in "([{":
+                depth += 1
+            elif ch in ")]}":
+                depth -= 1
+            elif ch == "," and depth == 1:
+                args += 1
+            if depth:
+                cur += ch
+            i += 1
+        out.append((m.group(1), 0 if not cur.strip() else args + 1))
+    return out
+
+
+def test_go_binding_matches_header_and_python_abi():
+    """go/crdtgpu/crdtgpu.go is never compiled here (no Go toolchain), so its
+    drift against the C ABI is checked by parsing: every C.crdt_* call passes
+    as many arguments as include/crdtgpu.h declares (and as crdtgpu/abi.py
+    binds, where both bind it); every field it names on a C.crdt_* struct --
+    in composite literals and on variables of those types -- is a field of
+    that struct in the header."""
+    import re
+
+    funcs, structs = _header_api()
+    assert {"crdt_awset_join_batch", "crdt_awset_exchange_batch", "crdt_awset_fold_batch"} <= set(funcs)
+    assert set(structs) >= {"crdt_awset_batch", "crdt_awset_out", "crdt_src_batch"}
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    go = open(os.path.join(root, "go", "crdtgpu", "crdtgpu.go")).read()
+    code = re.sub(r'//[^\n]*|"(?:[^"\\]|\\.)*"', "", go)
+    sigs = abi.signatures()
+    calls = _go_calls(code)
+    assert len(calls) >= 8
+    for name, n in calls:
+        assert name in funcs, name
+        assert n == funcs[name], "%s: Go passes %d arguments, the header declares %d" % (name, n, funcs[name])
+        if name in sigs:
+            assert len(sigs[name][1]) == n, "%s: abi.py binds %d arguments" % (name, len(sigs[name][1]))
+    # every Python binding agrees with the header too
+    for name, (_, args) in sigs.items():
+        assert funcs.get(name) == len(args), name
+    # struct fields in composite literals: C.crdt_x{field: ..., field: ...}
+    seen = 0
+    for m in re.finditer(r"\bC\.(crdt_\w+)\{", code):
+        i, depth, body = m.end(), 1, ""
+        while depth:
+            ch = code[i]
+            depth += ch == "{"
+            depth -= ch == "}"
+            if depth:
+                body += ch
+            i += 1
+        for f in re.findall(r"(?:^|[,{\s])(\w+)\s*:", body):
+            assert f in structs[m.group(1)], "%s has no field %s" % (m.group(1), f)
+            seen += 1
+    # fields on variables / struct members declared with a C.crdt_* struct type
+    bound = []  # (access pattern, struct): locals by name, struct members through their owner
+    for m in re.finditer(r"(\.?)\b(\w+)\s*(?::=|=)\s*C\.(crdt_\w+)\{", code):
+        owner = r"\w\." if m.group(1) else r"(?<![\w.])"
+        bound.append((r"%s%s\.([a-z_]\w*)" % (owner, m.group(2)), m.group(3)))
+    for m in re.finditer(r"^\s*(\w+)\s+C\.(crdt_\w+)\s*$", code, flags=re.M):
+        bound.append((r"\w\.%s\.([a-z_]\w*)" % m.group(1), m.group(2)))
+    for pat, st in bound:
+        if st not in structs:
+            continue
+        for f in re.findall(pat, code):
+            assert f in structs[st], "%s (%s) has no field %s" % (pat, st, f)
+            seen += 1
+    assert seen >= 20

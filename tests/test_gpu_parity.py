@@ -529,6 +529,70 @@ def test_gen_replicas_and_config5_fold(eng, torch):
     assert ctx.cpu().numpy().view(np.uint64).tolist() == oracle.causal_context(want.vv, n, R).tolist()
 
 
+def test_config5_bench_size(eng, torch):
+    """Config 5 exactly as bench.py times it on one GPU: 12,500,000 docs
+    (DEFAULT_DOCS[5], the bench seed 0x5EED of rank 0) x 8 replicas x 16
+    entries, R = 8, fold r0 <- r1 <- ... <- r7, then the causal-context summary.
+    - every 11th doc across the whole range (1,136,364 docs) plus the last one,
+      bit-exact vs the oracle run on the same device-generated inputs;
+    - every doc: its output clock is the u64 max of its 8 input clocks (each
+      step merges its source clock, awset.go:160 -> crdt-misc.go:43-55) and its
+      live count is <= 128;
+    - the summary crdt_causal_context_async over all 12.5 M outputs == the
+      oracle's max over the downloaded output clocks (crdt-misc.go:43-55)."""
+    n, P, E, R = 12_500_000, 8, 16, 8
+    dev = torch.device("cuda:0")
+    D = OutBuffers(n, R, n * E, device=dev)
+    S = SrcBuffers(R, n, n * (P - 1), n * (P - 1) * E, 0, device=dev)
+    eng.gen_replicas_async(0x5EED, n, P, E, D, S)
+    out = OutBuffers(n, R, n * E * P, device=dev)
+    eng.fold_async(CRDT_FOLD_AWSET, D.as_batch(), S, out)
+    ctx = torch.zeros(R, dtype=torch.int64, device=dev)
+    eng.causal_context_async(out.vv, n, R, ctx)
+    eng.sync()
+    torch.cuda.synchronize()
+    ar = torch.arange(n + 1, dtype=torch.int64, device=dev)
+    # the generator's and the fold's fixed slot layout, which the gathers below rely on
+    assert bool((D.offsets.to(torch.int64) == ar * E).all())
+    assert bool((S.doc_srcs.to(torch.int64) == ar * (P - 1)).all())
+    assert bool((S.entry_off.to(torch.int64) == torch.arange(n * (P - 1) + 1, device=dev) * E).all())
+    assert bool((out.offsets.to(torch.int64) == ar * E * P).all())
+    # every doc: output clock == u64 max of the input clocks; live count within capacity
+    flip = torch.tensor(-(1 << 63), dtype=torch.int64, device=dev)
+    vin = torch.maximum(D.vv.view(n, R) ^ flip, (S.vv.view(n, P - 1, R) ^ flip).amax(dim=1))
+    assert bool(((out.vv.view(n, R) ^ flip) == vin).all()), "output clock != max of input clocks"
+    del vin
+    assert int(out.counts.max()) <= E * P and int(out.counts.min()) >= 0
+    # the strided sample, gathered on the device into a batch of its own
+    docs = torch.cat([torch.arange(0, n, 11, device=dev), torch.tensor([n - 1], device=dev)])
+    m = int(docs.numel())
+    assert m >= 1 << 20
+    u32, u64 = np.uint32, np.uint64
+
+    def rows(t, w, dt):
+        return t[: n * w].view(n, w).index_select(0, docs).reshape(-1).cpu().numpy().view(dt)
+
+    hd = AWSetBatch(R, np.arange(m + 1, dtype=u32) * E, rows(D.keys, E, u64), rows(D.actors, E, u32),
+                    rows(D.counters, E, u64), rows(D.vv, R, u64), counts=rows(D.counts, 1, u32))
+    ns = m * (P - 1)
+    hs = SrcBatch(R, np.arange(m + 1, dtype=u32) * (P - 1), rows(S.src_actor, P - 1, u32),
+                  rows(S.vv, (P - 1) * R, u64), np.arange(ns + 1, dtype=u32) * E,
+                  rows(S.keys, (P - 1) * E, u64), rows(S.actors, (P - 1) * E, u32),
+                  rows(S.counters, (P - 1) * E, u64), np.zeros(ns + 1, dtype=u32), np.zeros(1, dtype=u64),
+                  np.zeros(1, dtype=u32), np.zeros(1, dtype=u64))
+    got = OutBuffers(m, R, 0)
+    got.offsets = np.arange(m + 1, dtype=u32) * E * P
+    got.counts = rows(out.counts, 1, u32)
+    got.keys, got.actors = rows(out.keys, E * P, u64), rows(out.actors, E * P, u32)
+    got.counters, got.vv = rows(out.counters, E * P, u64), rows(out.vv, R, u64)
+    rc, want = oracle.fold(CRDT_FOLD_AWSET, hd, hs)
+    assert rc == 0
+    assert_same_all(got, want, m, R)
+    # the summary over all 12.5 M docs
+    all_vv = out.vv[: n * R].cpu().numpy().view(u64)
+    assert ctx.cpu().numpy().view(u64).tolist() == oracle.causal_context(all_vv, n, R).tolist()
+
+
 def gen_zipf(eng, torch, n, seed=0x5EED):
     from crdtgpu.engine import zipf_sizes
 
@@ -657,11 +721,13 @@ def test_exchange_equals_two_joins(eng, torch, sizes):
     assert_same(o2, w2, a.n_docs, R)
 
 
-@pytest.mark.parametrize("stage,shared", [(1, 0), (1, 1), (0, 0), (0, 1)])
-def test_exchange_config2_full_size(eng, torch, stage, shared):
+@pytest.mark.parametrize("stage,shared,slab", [(1, 0, 0), (1, 1, 0), (0, 0, 0), (0, 1, 0), (1, 1, 7)])
+def test_exchange_config2_full_size(eng, torch, stage, shared, slab):
     """All 1,048,576 config-2 docs, both directions, vs the oracle joins: LDS-
     staged contiguous stores (the default) and the lane-scattered stores, each
-    with its own and with one shared key column (out_ba.keys = out_ab.keys)."""
+    with its own and with one shared key column (out_ba.keys = out_ab.keys);
+    and the slab block order (join_slab_blocks_per_cu = 7: blocks remapped to
+    contiguous chunks per CU, padding blocks exiting at once)."""
     n = 1 << 20
     A, B = gen_pair(eng, torch, n, 0x5EED)
     dev = torch.device("cuda:0")
@@ -669,12 +735,14 @@ def test_exchange_config2_full_size(eng, torch, stage, shared):
     oba = OutBuffers(n, 2, 2 * n * 64, device=dev, shared_keys=oab if shared else None)
     eng.set_max_doc_entries(64)
     eng.set_option("join_stage_stores", stage)
+    eng.set_option("join_slab_blocks_per_cu", slab)
     try:
         eng.exchange_async(A.as_batch(), B.as_batch(), oab, oba)
         eng.sync()
     finally:
         eng.set_max_doc_entries()
         eng.set_option("join_stage_stores", 1)
+        eng.set_option("join_slab_blocks_per_cu", 0)
     ha, hb = host_out(A, torch).as_batch(), host_out(B, torch).as_batch()
     rc, want = oracle.join(ha, hb)
     assert rc == 0
@@ -682,6 +750,35 @@ def test_exchange_config2_full_size(eng, torch, stage, shared):
     rc, want = oracle.join(hb, ha)
     assert rc == 0
     assert_same_all(host_out(oba, torch), want, n, 2)
+
+
+def test_exchange_rejects_overlapping_outputs(eng, torch):
+    """crdt_awset_exchange_async: only keys == keys may be shared; two arrays at
+    one address, or per-document arrays overlapping, are CRDT_E_INVALID."""
+    n, R = 64, 2
+    dev = torch.device("cuda:0")
+    A, B = gen_pair(eng, torch, n, 7)
+    o1 = OutBuffers(n, R, 2 * n * 64, device=dev)
+    big = torch.empty(3 * n * R, dtype=torch.int64, device=dev)
+    cases = {
+        "actors": lambda o2: setattr(o2, "actors", o1.actors),
+        "keys=counters": lambda o2: setattr(o2, "counters", o1.keys),
+        "vv partial": None,
+        "offsets=counts": lambda o2: setattr(o2, "offsets", o1.counts),
+    }
+    for what, mut in cases.items():
+        o2 = OutBuffers(n, R, 2 * n * 64, device=dev)
+        if mut is None:  # two VV arrays overlapping by one document
+            o1v, o2.vv = o1.vv, big[(n - 1) * R:]
+            o1.vv = big[: n * R]
+        else:
+            mut(o2)
+        with pytest.raises(crdtgpu.CrdtError) as ei:
+            eng.exchange_async(A.as_batch(), B.as_batch(), o1, o2)
+        assert ei.value.code == crdtgpu.CRDT_E_INVALID, what
+        if mut is None:
+            o1.vv = o1v
+    eng.sync()
 
 
 @pytest.mark.parametrize("packed", [0, 1])

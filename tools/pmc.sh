@@ -1,16 +1,29 @@
 #!/bin/bash
-# PMC passes for the join kernel, one counter group per rocprofv3 run (gfx950
+# PMC passes for one bench config, one counter group per rocprofv3 run (gfx950
 # slot limits), plus the known-byte calibration run.  GPU box only.
+#
+#   CONFIG=2|3|4|5 TAG=r05x bash tools/pmc.sh
+#
+# Writes gpurun_out/pmc_$TAG/summary.txt and adds the entry (exact kernel
+# instance + source id, tools/traffic.py) to profiles/traffic.json.
 set -u
 cd "$(dirname "$0")/.."
-TAG=${TAG:-r01}
+TAG=${TAG:-r05}
+CONFIG=${CONFIG:-2}
 OUT=gpurun_out/pmc_$TAG
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
-BENCH="python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline ${BENCH_ARGS:-}"
+case $CONFIG in
+  2) KERNEL=${KERNEL:-"join_wave_kernel<4, 8, 2, true, true>"}; TUS=join.hip; DOCS=1048576; STEPS=3 ;;
+  3) KERNEL=${KERNEL:-"fold_pipe_kernel<16, true, true, false>"}; TUS=fold.hip; DOCS=1048576; STEPS=2 ;;
+  4) KERNEL=${KERNEL:-"join_tile_pipe_kernel<512, 2, true, true, true>"}; TUS=join.hip,tile.hip; DOCS=16384; STEPS=2 ;;
+  5) KERNEL=${KERNEL:-"fold_pipe_kernel<32, false, true, false>"}; TUS=fold.hip; DOCS=12500000; STEPS=2 ;;
+  *) echo "CONFIG must be 2..5"; exit 2 ;;
+esac
+BENCH="python3 bench.py --config $CONFIG --legs none --steps $STEPS --warmup 1 --repeats 1 --no-cpu-baseline --no-box-probe --no-sort --no-boundary ${BENCH_ARGS:-}"
 pass() {
   local name=$1; shift
-  timeout -k 10 -s KILL 120 rocprofv3 --pmc "$@" --output-format csv -d "$OUT/$name" -o run -- $BENCH > "$OUT/$name.log" 2>&1
+  timeout -k 10 -s KILL 150 rocprofv3 --pmc "$@" --output-format csv -d "$OUT/$name" -o run -- $BENCH > "$OUT/$name.log" 2>&1
   local rc=$?; echo "[pmc $name] rc=$rc"; [ $rc -eq 0 ] || { tail -20 "$OUT/$name.log"; exit $rc; }
 }
 cpass() {
@@ -18,26 +31,18 @@ cpass() {
   timeout -k 10 -s KILL 120 rocprofv3 --pmc "$@" --output-format csv -d "$OUT/$name" -o run -- python3 tools/calib.py > "$OUT/$name.log" 2>&1
   local rc=$?; echo "[pmc $name] rc=$rc"; [ $rc -eq 0 ] || { tail -20 "$OUT/$name.log"; exit $rc; }
 }
-if [ "${FOLD:-0}" = 1 ]; then
-  BENCH="python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline ${BENCH_ARGS:-}"
-  pass sq SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU
-  pass lds SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_SALU SQ_INSTS_SMEM SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS GRBM_GUI_ACTIVE GRBM_COUNT
-  pass lds2 SQ_LDS_IDX_ACTIVE SQ_LDS_ADDR_CONFLICT SQ_LDS_UNALIGNED_STALL SQ_INSTS_VMEM SQ_INST_LEVEL_LDS SQ_ACCUM_PREV_HIRES
-  pass fetch FETCH_SIZE
-  pass write WRITE_SIZE
-  cpass calib_fetch FETCH_SIZE
-  cpass calib_write WRITE_SIZE
-  python3 tools/traffic.py "$OUT" --docs ${DOCS:-1048576} --config ${CONFIG:-3} --kernel "${KERNEL:-fold_pipe_kernel}" --emit > "$OUT/summary.txt"; cat "$OUT/summary.txt"
-  exit 0
-fi
 pass fetch FETCH_SIZE
 pass write WRITE_SIZE
 pass sq SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU
 pass lds SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_SALU SQ_INSTS_SMEM SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS GRBM_GUI_ACTIVE GRBM_COUNT
-pass tcc TCC_HIT_sum TCC_MISS_sum
+pass tcc TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum
+if [ "${EXTRA:-0}" = 1 ]; then
+  pass lds2 SQ_LDS_IDX_ACTIVE SQ_LDS_ADDR_CONFLICT SQ_LDS_UNALIGNED_STALL SQ_INSTS_VMEM SQ_INST_LEVEL_LDS SQ_ACCUM_PREV_HIRES
+fi
 cpass calib_fetch FETCH_SIZE
 cpass calib_write WRITE_SIZE
-# the bench's exchange shares one key column between its outputs unless BENCH_ARGS has --own-keys
-case "${BENCH_ARGS:-}" in *--own-keys*) SK=0 ;; *) SK=1 ;; esac
-python3 tools/traffic.py "$OUT" --docs ${DOCS:-1048576} --config ${CONFIG:-2} --kernel "${KERNEL:-join_wave_kernel}" \
-  --shared-keys $SK --emit > "$OUT/summary.txt" && cat "$OUT/summary.txt"
+# the bench's config-2 exchange shares one key column between its outputs unless BENCH_ARGS has --own-keys
+SK=0
+if [ "$CONFIG" = 2 ]; then case "${BENCH_ARGS:-}" in *--own-keys*) SK=0 ;; *) SK=1 ;; esac; fi
+python3 tools/traffic.py "$OUT" --docs $DOCS --config $CONFIG --kernel "$KERNEL" --tus $TUS --shared-keys $SK \
+  --profile "profiles/${TAG}_pmc_summary.txt" --emit > "$OUT/summary.txt" && cat "$OUT/summary.txt"

@@ -43,6 +43,8 @@ def main():
     ap.add_argument("--config", type=int, default=2)
     ap.add_argument("--kernel", default="join_wave_kernel")
     ap.add_argument("--shared-keys", type=int, default=0, help="exchange runs: the two outputs shared one key column")
+    ap.add_argument("--tus", default="join.hip", help="comma-separated translation units of the kernel (crdtgpu.srcid)")
+    ap.add_argument("--profile", default="", help="the profiles/ summary this entry is committed as")
     a = ap.parse_args()
     out, calib = {}, {}
     for sub in sorted(os.listdir(a.dir)):
@@ -62,9 +64,17 @@ def main():
     N = 64 << 20
     fcorr = (16 * N) / (cal["FETCH_SIZE"] * 1024) if cal.get("FETCH_SIZE") else None
     wcorr = (8 * N) / (cal["WRITE_SIZE"] * 1024) if cal.get("WRITE_SIZE") else None
-    jk = next((k for k in out if k.startswith(a.kernel)), "")
+    # the exact instance when --kernel names one (has '<'), else the first of the family
+    jk = a.kernel if "<" in a.kernel else next((k for k in out if k.startswith(a.kernel)), "")
     j = out.get(jk, {})
-    res = {"docs": a.docs, "config": a.config, "kernel": jk, "exchange": jk.startswith("join") and jk.endswith("true>"),
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "go-crdt-playground_amd"))
+    from crdtgpu.srcid import source_id
+
+    exch = jk.startswith("join") and (jk.split(",")[3:4] == [" true"] if "tile" not in jk else
+                                       jk.split(",")[2:3] == [" true"])
+    res = {"docs": a.docs, "config": a.config, "kernel": jk, "exchange": exch,
+           "src_id": source_id(tuple(x for x in a.tus.split(",") if x)), "profile": a.profile,
            "fetch_correction": fcorr, "write_correction": wcorr}
     if res["exchange"]:
         res["shared_keys"] = bool(a.shared_keys)
