@@ -17,14 +17,23 @@
 
 namespace crdt {
 
+// CRDT_JOIN_PAD_STORES (diagnostic build option): the staged stores (STG) of
+// each output array run on past the last survivor to the end of its cache
+// line, within the document's own output capacity, so no line of a document's
+// output is written partially (what they write past the live count is slack,
+// whose contents the ABI leaves unspecified).
+#ifndef CRDT_JOIN_PAD_STORES
+#define CRDT_JOIN_PAD_STORES 0
+#endif
+
 struct JoinMeta {
-    uint32_t doff, soff, dn, sn;
+    uint32_t doff, soff, dn, sn, cap;
 };
 
 // Metadata of up to 64 documents, lane i = document first + i*stride: one
 // unconditional vector load per field (indices clamped).
 struct MetaVec {
-    uint32_t doff, soff, dend, send;
+    uint32_t doff, soff, dend, send, dnx, snx;
 };
 
 __device__ __forceinline__ MetaVec meta_vec_issue(const BatchView& dst, const BatchView& src, uint32_t first,
@@ -37,6 +46,12 @@ __device__ __forceinline__ MetaVec meta_vec_issue(const BatchView& dst, const Ba
     v.soff = src.offsets[dd];
     v.dend = dst.counts ? dst.counts[dd] : dst.offsets[dd + 1];
     v.send = src.counts ? src.counts[dd] : src.offsets[dd + 1];
+    if (CRDT_JOIN_PAD_STORES) {  // slot bounds of the next document: the output capacity
+        v.dnx = dst.counts ? dst.offsets[dd + 1] : v.dend;
+        v.snx = src.counts ? src.offsets[dd + 1] : v.send;
+    } else {
+        v.dnx = v.snx = 0;
+    }
     return v;
 }
 
@@ -49,6 +64,10 @@ __device__ __forceinline__ JoinMeta meta_of(const BatchView& dst, const BatchVie
     const uint32_t b = (uint32_t)__builtin_amdgcn_readlane((int)v.send, (int)i);
     m.dn = dst.counts ? a : a - m.doff;
     m.sn = src.counts ? b : b - m.soff;
+    m.cap = 0;
+    if (CRDT_JOIN_PAD_STORES)
+        m.cap = (uint32_t)__builtin_amdgcn_readlane((int)v.dnx, (int)i) - m.doff +
+                (uint32_t)__builtin_amdgcn_readlane((int)v.snx, (int)i) - m.soff;
     return m;
 }
 
@@ -158,9 +177,19 @@ __device__ __forceinline__ void join_doc(JoinWaveSmem<WAVES>& sm, uint32_t w, co
         wave_sync();
         const uint64_t k0 = ik[lane], k1 = ik[lane + 64], c0 = ic[lane], c1 = ic[lane + 64];
         const uint32_t a0 = ia[lane], a1 = ia[lane + 64];
-        const rsrc_t ok = make_rsrc(out.keys + obase, n_out * 8u);
-        const rsrc_t oa = make_rsrc(out.actors + obase, n_out * 4u);
-        const rsrc_t oc = make_rsrc(out.counters + obase, n_out * 8u);
+        // slots each array's stores cover: the survivors, or (padded) through
+        // the end of the last survivor's cache line, within the capacity
+        uint32_t n8 = n_out, n4 = n_out;
+        if (CRDT_JOIN_PAD_STORES && small && n_out != 0) {  // (a large document: the block / tile path writes it)
+            const uint32_t lim = min(m.cap, 128u);
+            n8 = min(((obase + n_out + 15u) & ~15u) - obase, lim);
+            n4 = min(((obase + n_out + 31u) & ~31u) - obase, lim);
+            n8 = max(n8, n_out);
+            n4 = max(n4, n_out);
+        }
+        const rsrc_t ok = make_rsrc(out.keys + obase, n8 * 8u);
+        const rsrc_t oa = make_rsrc(out.actors + obase, n4 * 4u);
+        const rsrc_t oc = make_rsrc(out.counters + obase, n8 * 8u);
         st64<AUX>(k0, ok, lane * 8u);
         st64<AUX>(k1, ok, lane * 8u + 512u);
         st32<AUX>(a0, oa, lane * 4u);
@@ -177,9 +206,9 @@ __device__ __forceinline__ void join_doc(JoinWaveSmem<WAVES>& sm, uint32_t w, co
             wave_sync();
             const uint64_t e0 = ic[lane], e1 = ic[lane + 64];
             const uint32_t b0 = ia[lane], b1 = ia[lane + 64];
-            const rsrc_t pk = make_rsrc(out2.keys + obase, kshare ? 0u : n_out * 8u);
-            const rsrc_t pa = make_rsrc(out2.actors + obase, n_out * 4u);
-            const rsrc_t pc = make_rsrc(out2.counters + obase, n_out * 8u);
+            const rsrc_t pk = make_rsrc(out2.keys + obase, kshare ? 0u : n8 * 8u);
+            const rsrc_t pa = make_rsrc(out2.actors + obase, n4 * 4u);
+            const rsrc_t pc = make_rsrc(out2.counters + obase, n8 * 8u);
             if (!kshare) {
                 st64<AUX>(k0, pk, lane * 8u);
                 st64<AUX>(k1, pk, lane * 8u + 512u);

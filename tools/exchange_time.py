@@ -19,12 +19,19 @@ eng = crdtgpu.Engine(0)
 eng.set_max_doc_entries(64)
 A, B = OutBuffers(n, 2, n * 64, device=dev), OutBuffers(n, 2, n * 64, device=dev)
 eng.gen_pair_async(0x5EED, n, A, B)
-o1, o2 = OutBuffers(n, 2, 2 * n * 64, device=dev), OutBuffers(n, 2, 2 * n * 64, device=dev)
+o1 = OutBuffers(n, 2, 2 * n * 64, device=dev)
+# the bench's form: one key column shared by the two outputs (OWN_KEYS=1: one each)
+o2 = OutBuffers(n, 2, 2 * n * 64, device=dev, shared_keys=None if os.environ.get("OWN_KEYS") == "1" else o1)
 a, b = A.as_batch(), B.as_batch()
 s = torch.cuda.current_stream()
 eng.exchange_async(a, b, o1, o2, stream=s)
 eng.sync()
-chk = int(o1.keys.sum()) ^ int(o2.counters.sum()) ^ int(o1.counts.to(torch.int64).sum())
+# checksum of the live entries only (slack slots are unspecified: variants may write them)
+live = (torch.arange(128, device=dev).view(1, 128) < o1.counts.to(torch.int64).view(n, 1)).view(-1)
+chk = (int(o1.keys[live].sum()) ^ int(o2.counters[live].sum()) ^ int(o1.actors[live].to(torch.int64).sum() << 20)
+       ^ int(o2.actors[live].to(torch.int64).sum() << 40) ^ int(o1.counters[live].sum()) ^ int(o1.vv.sum())
+       ^ int(o1.counts.to(torch.int64).sum()))
+assert bool((o1.offsets[:n].to(torch.int64) == torch.arange(n, device=dev) * 128).all())
 ts = []
 for _ in range(6):
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

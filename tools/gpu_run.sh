@@ -79,6 +79,13 @@ for r in "$@"; do
       TAILN=1 step bsdma_off_$TAG 200 env HSA_ENABLE_SDMA=0 CRDT_TRACE_STAGE=1 go-crdt-playground_amd/host/build/boundary_bench 65536
       TAILN=1 step bsdma_on_$TAG 200 env CRDT_TRACE_STAGE=1 go-crdt-playground_amd/host/build/boundary_bench 65536
       TAILN=1 step bsdma_off2_$TAG 200 env HSA_ENABLE_SDMA=0 go-crdt-playground_amd/host/build/boundary_bench 65536 ;;
+    bmalloc)
+      # is the boundary's blocking first copy the C library returning freed heap to the OS
+      # (munmap / madvise -> the GPU driver's MMU-notifier invalidations) during pack/apply?
+      TAILN=40 step bmalloc_default_$TAG 200 env CRDT_TRACE_STAGE=1 go-crdt-playground_amd/host/build/boundary_bench 65536
+      TAILN=40 step bmalloc_keep_$TAG 200 env CRDT_TRACE_STAGE=1 MALLOC_TRIM_THRESHOLD_=68719476736 MALLOC_MMAP_THRESHOLD_=33554432 MALLOC_TOP_PAD_=1073741824 go-crdt-playground_amd/host/build/boundary_bench 65536
+      TAILN=2 step bmalloc_keep2_$TAG 200 env MALLOC_TRIM_THRESHOLD_=68719476736 MALLOC_MMAP_THRESHOLD_=33554432 MALLOC_TOP_PAD_=1073741824 go-crdt-playground_amd/host/build/boundary_bench 65536
+      TAILN=2 step bmalloc_default2_$TAG 200 env go-crdt-playground_amd/host/build/boundary_bench 65536 ;;
     btrace)
       TAILN=30 step bplain_$TAG 200 env CRDT_TRACE_STAGE=1 go-crdt-playground_amd/host/build/boundary_bench 65536
       CRDT_TRACE_STAGE=1 TAILN=10 step btrace_$TAG 300 rocprofv3 --hip-trace --memory-copy-trace --kernel-trace --stats \
