@@ -99,6 +99,13 @@ namespace crdt {
 #ifndef CRDT_FOLD_NO_STORES
 #define CRDT_FOLD_NO_STORES 0
 #endif
+// CRDT_FOLD_PAD_STORES (with CRDT_FOLD_STAGE_STORES 1, diagnostic): each array's
+// staged stores run on to the end of the last survivor's cache line, within
+// the document's output capacity (slack past the live count is unspecified),
+// so no output line is written partially.
+#ifndef CRDT_FOLD_PAD_STORES
+#define CRDT_FOLD_PAD_STORES 0
+#endif
 #ifndef CRDT_FOLD_PURE_CHUNKS
 #define CRDT_FOLD_PURE_CHUNKS 0
 #endif
@@ -1534,9 +1541,15 @@ __global__ __launch_bounds__(fold_waves<DELTA>() * 64) __attribute__((amdgpu_wav
                 __builtin_amdgcn_raw_buffer_store_b128(av, sa, (int)(in ? i * 4u : kOOB), 0, kFoldStoreAux);
             }
         } else {
-            const rsrc_t sk = make_rsrc(out.keys + obase, min(U, capo) * 8u);
-            const rsrc_t sa = make_rsrc(out.actors + obase, min(U, capo) * 4u);
-            const rsrc_t sc = make_rsrc(out.counters + obase, min(U, capo) * 8u);
+            const uint32_t nw = min(U, capo);
+            uint32_t n8 = nw, n4 = nw;
+            if (CRDT_FOLD_PAD_STORES && nw != 0) {
+                n8 = min(((obase + nw + 15u) & ~15u) - obase, capo);
+                n4 = min(((obase + nw + 31u) & ~31u) - obase, capo);
+            }
+            const rsrc_t sk = make_rsrc(out.keys + obase, n8 * 8u);
+            const rsrc_t sa = make_rsrc(out.actors + obase, n4 * 4u);
+            const rsrc_t sc = make_rsrc(out.counters + obase, n8 * 8u);
 #pragma unroll
             for (int q = 0; q < NCH; ++q) {
                 const uint32_t i = q * 64u + lane;

@@ -21,16 +21,22 @@
 
 using namespace crdt;
 
-// order-independent checksum of an output (every slot; the buffers are zeroed
-// first, so slack slots hash the same in every build): variants of the fold
-// must print the same value
-__global__ void checksum_kernel(const uint32_t* counts, const uint64_t* vv, size_t n_vv, const uint64_t* keys,
-                                const uint32_t* actors, const uint64_t* ctrs, size_t slots, uint32_t n,
+// order-independent checksum of an output (the live entries of every document,
+// their slot bounds, counts and clocks; slack slots are unspecified and some
+// variants write them): variants of the fold must print the same value
+__global__ void checksum_kernel(const uint32_t* offsets, const uint32_t* counts, const uint64_t* vv, size_t n_vv,
+                                const uint64_t* keys, const uint32_t* actors, const uint64_t* ctrs, uint32_t n,
                                 unsigned long long* out) {
     unsigned long long h = 0;
     const size_t stride = (size_t)gridDim.x * blockDim.x;
-    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < slots; i += stride)
-        h += (keys[i] * 0x9E3779B97F4A7C15ull) ^ (ctrs[i] * 0xC2B2AE3D27D4EB4Full) ^ ((uint64_t)actors[i] << 17) ^ i;
+    for (size_t d = blockIdx.x * (size_t)blockDim.x + threadIdx.x; d < n; d += stride) {
+        const size_t o = offsets[d];
+        h += o * 0x2545F4914F6CDD1Dull;
+        for (uint32_t j = 0; j < counts[d]; ++j) {
+            const size_t i = o + j;
+            h += (keys[i] * 0x9E3779B97F4A7C15ull) ^ (ctrs[i] * 0xC2B2AE3D27D4EB4Full) ^ ((uint64_t)actors[i] << 17) ^ i;
+        }
+    }
     for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n_vv; i += stride)
         h += (vv[i] + 0x165667B19E3779F9ull) * (i + 1);
     for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += stride) h += (uint64_t)counts[i] << (i & 31);
@@ -115,8 +121,8 @@ int main(int argc, char** argv) {
     CK(hipMemcpy(&status, ws + 16, 4, hipMemcpyDeviceToHost));
     unsigned long long* dsum = dalloc<unsigned long long>(1);
     CK(hipMemset(dsum, 0, 8));
-    hipLaunchKernelGGL(checksum_kernel, dim3(4096), dim3(256), 0, 0, O.counts, O.vv, (size_t)n * R, O.keys, O.actors,
-                       O.counters, oslots, n, dsum);
+    hipLaunchKernelGGL(checksum_kernel, dim3(4096), dim3(256), 0, 0, O.offsets, O.counts, O.vv, (size_t)n * R, O.keys,
+                       O.actors, O.counters, n, dsum);
     unsigned long long hsum = 0;
     CK(hipMemcpy(&hsum, dsum, 8, hipMemcpyDeviceToHost));
     printf("output checksum %016llx\n", hsum);
