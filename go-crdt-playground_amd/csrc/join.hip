@@ -17,13 +17,17 @@
 
 namespace crdt {
 
-// CRDT_JOIN_PAD_STORES (diagnostic build option): the staged stores (STG) of
-// each output array run on past the last survivor to the end of its cache
-// line, within the document's own output capacity, so no line of a document's
-// output is written partially (what they write past the live count is slack,
-// whose contents the ABI leaves unspecified).
+// CRDT_JOIN_PAD_STORES (default on): the staged stores (STG) of each output
+// array run on past the last survivor to the end of its cache line, within
+// the document's own output capacity, writing zeros there (slack slots, whose
+// contents the ABI leaves unspecified), so no line of a document's output is
+// written partially.  A partially written line costs the memory more than a
+// whole one: the config-2 exchange 1.216 -> 1.124 ms per launch (-7.6 %, same
+// box, three interleaved rounds, identical live outputs; profiles/r05b_*).
+// The folds gain nothing from it (their stores are not what binds them:
+// profiles/r05b_*), so they keep their own store forms.
 #ifndef CRDT_JOIN_PAD_STORES
-#define CRDT_JOIN_PAD_STORES 0
+#define CRDT_JOIN_PAD_STORES 1
 #endif
 
 struct JoinMeta {
@@ -175,8 +179,11 @@ __device__ __forceinline__ void join_doc(JoinWaveSmem<WAVES>& sm, uint32_t w, co
             ia[spos] = L.sa;
         }
         wave_sync();
-        const uint64_t k0 = ik[lane], k1 = ik[lane + 64], c0 = ic[lane], c1 = ic[lane + 64];
-        const uint32_t a0 = ia[lane], a1 = ia[lane + 64];
+        // (slots past the survivors read as 0: the padding below writes zeros)
+        const bool l0 = lane < n_out, l1 = lane + 64u < n_out;
+        const uint64_t k0 = l0 ? ik[lane] : 0ull, k1 = l1 ? ik[lane + 64] : 0ull;
+        const uint64_t c0 = l0 ? ic[lane] : 0ull, c1 = l1 ? ic[lane + 64] : 0ull;
+        const uint32_t a0 = l0 ? ia[lane] : 0u, a1 = l1 ? ia[lane + 64] : 0u;
         // slots each array's stores cover: the survivors, or (padded) through
         // the end of the last survivor's cache line, within the capacity
         uint32_t n8 = n_out, n4 = n_out;
@@ -204,8 +211,8 @@ __device__ __forceinline__ void join_doc(JoinWaveSmem<WAVES>& sm, uint32_t w, co
                 ia[dpos] = L.da;
             }
             wave_sync();
-            const uint64_t e0 = ic[lane], e1 = ic[lane + 64];
-            const uint32_t b0 = ia[lane], b1 = ia[lane + 64];
+            const uint64_t e0 = l0 ? ic[lane] : 0ull, e1 = l1 ? ic[lane + 64] : 0ull;
+            const uint32_t b0 = l0 ? ia[lane] : 0u, b1 = l1 ? ia[lane + 64] : 0u;
             const rsrc_t pk = make_rsrc(out2.keys + obase, kshare ? 0u : n8 * 8u);
             const rsrc_t pa = make_rsrc(out2.actors + obase, n4 * 4u);
             const rsrc_t pc = make_rsrc(out2.counters + obase, n8 * 8u);
