@@ -189,8 +189,10 @@ __device__ __forceinline__ void join_doc(JoinWaveSmem<WAVES>& sm, uint32_t w, co
         uint32_t n8 = n_out, n4 = n_out;
         if (CRDT_JOIN_PAD_STORES && small && n_out != 0) {  // (a large document: the block / tile path writes it)
             const uint32_t lim = min(m.cap, 128u);
-            n8 = min(((obase + n_out + 15u) & ~15u) - obase, lim);
-            n4 = min(((obase + n_out + 31u) & ~31u) - obase, lim);
+            // 1: whole 128-byte lines; 2 (diagnostic): 64-byte halves
+            constexpr uint32_t m8 = CRDT_JOIN_PAD_STORES == 2 ? 7u : 15u, m4 = CRDT_JOIN_PAD_STORES == 2 ? 15u : 31u;
+            n8 = min(((obase + n_out + m8) & ~m8) - obase, lim);
+            n4 = min(((obase + n_out + m4) & ~m4) - obase, lim);
             n8 = max(n8, n_out);
             n4 = max(n4, n_out);
         }
