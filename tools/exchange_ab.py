@@ -28,14 +28,16 @@ o1 = OutBuffers(n, 2, 2 * n * 64, device=dev)
 o2 = OutBuffers(n, 2, 2 * n * 64, device=dev)
 o2s = OutBuffers(n, 2, 2 * n * 64, device=dev, shared_keys=o1)
 s = torch.cuda.current_stream()
-forms = [tuple(int(x) for x in (f + ",8").split(",")[:4]) for f in os.environ.get(
-    "FORMS", "1,1,0;1,1,7;1,1,14;1,1,4;1,0,0;1,0,7").split(";")]  # stage, shared, slab[, docs per wave]
+_DEF = (1, 1, 0, 8, 1)
+forms = [tuple([int(x) for x in f.split(",")] + list(_DEF[len(f.split(",")):]))
+         for f in os.environ.get("FORMS", "1,1,0;1,1,7;1,1,14;1,1,4;1,0,0;1,0,7").split(";")]
 
 
 def run(form, reps):
     eng.set_option("join_stage_stores", form[0])
     eng.set_option("join_slab_blocks_per_cu", form[2])
     eng.set_option("join_docs_per_wave", form[3])
+    eng.set_option("join_nt_stores", form[4])
     eng.exchange_async(a, b, o1, o2s if form[1] else o2, stream=s)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record(s)
@@ -80,11 +82,12 @@ for f in forms:
     med = v[len(v) // 2]
     # bytes: inputs 20 B/entry, out1 20 B/entry, out2 20 (own keys) or 12 B/entry, VVs/offsets/counts
     byt = 20 * n_in + (20 + (12 if f[1] else 20)) * n_out + n * (2 * 2 * 8 + 2 * 2 * 8 + 2 * 8 + 2 * 8)
-    print("stage=%d shared_keys=%d slab=%-2d K=%-2d median %.4f ms  min %.4f ms  %.0f GB/s algorithmic (%.3f GB)  same=%s" % (
-        f[0], f[1], f[2], f[3], med, v[0], byt / med / 1e6, byt / 1e9, same[f]))
+    print("stage=%d shared_keys=%d slab=%-2d K=%-2d nt=%d median %.4f ms  min %.4f ms  %.0f GB/s algorithmic (%.3f GB)  "
+          "same=%s" % (f[0], f[1], f[2], f[3], f[4], med, v[0], byt / med / 1e6, byt / 1e9, same[f]))
 eng.set_option("join_stage_stores", 1)
 eng.set_option("join_slab_blocks_per_cu", 0)
 eng.set_option("join_docs_per_wave", 8)
+eng.set_option("join_nt_stores", 1)
 del o1, o2, o2s, A, B
 torch.cuda.empty_cache()
 x = torch.empty(2 << 30, dtype=torch.uint8, device=dev)
