@@ -115,6 +115,7 @@ struct TileWork {
     uint32_t tile;   // merged positions per tile (= the tile kernel's NT * IPT)
     uint32_t shape;  // tile kernel shape (tile.hip, tile_positions)
     uint32_t nt_stores;  // non-temporal output stores ("join_tile_nt_stores")
+    uint32_t split_bpc;  // tile_split_kernel workgroups per CU ("join_tile_split_blocks_per_cu")
 };
 
 // ---- slab order of a grid's blocks.  A streaming kernel whose concurrently

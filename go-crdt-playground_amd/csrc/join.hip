@@ -17,15 +17,18 @@
 
 namespace crdt {
 
-// CRDT_JOIN_PAD_STORES (default on): the staged stores (STG) of each output
-// array run on past the last survivor to the end of its cache line, within
-// the document's own output capacity, writing zeros there (slack slots, whose
-// contents the ABI leaves unspecified), so no line of a document's output is
-// written partially.  A partially written line costs the memory more than a
-// whole one: the config-2 exchange 1.216 -> 1.124 ms per launch (-7.6 %, same
-// box, three interleaved rounds, identical live outputs; profiles/r05b_*).
-// The folds gain nothing from it (their stores are not what binds them:
-// profiles/r05b_*), so they keep their own store forms.
+// CRDT_JOIN_PAD_STORES (default 1): the staged stores (STG) of each output
+// array run on past the last survivor to the end of its 64-byte sector,
+// within the document's own output capacity, writing zeros there (slack
+// slots, whose contents the ABI leaves unspecified), so no sector of a
+// document's output is written partially.  A partially written sector costs
+// the memory far more than its bytes: the config-2 exchange 1.216 -> 1.124 ms
+// per launch padded to 128-byte lines (-7.6 %, three interleaved rounds,
+// identical live outputs; profiles/r05b_exchange_pad_ab.log), 1.125 -> 1.108
+// ms more padded to 64-byte sectors (profiles/r05d_exchange_pad_ab.log; 2 =
+// 128-byte lines, 0 = off).  The folds gain nothing from it (their stores are
+// not what binds them: profiles/r05b_fold_stage_pad_ab.log), so they keep
+// their own store forms.
 #ifndef CRDT_JOIN_PAD_STORES
 #define CRDT_JOIN_PAD_STORES 1
 #endif
@@ -189,8 +192,8 @@ __device__ __forceinline__ void join_doc(JoinWaveSmem<WAVES>& sm, uint32_t w, co
         uint32_t n8 = n_out, n4 = n_out;
         if (CRDT_JOIN_PAD_STORES && small && n_out != 0) {  // (a large document: the block / tile path writes it)
             const uint32_t lim = min(m.cap, 128u);
-            // 1: whole 128-byte lines; 2 (diagnostic): 64-byte halves
-            constexpr uint32_t m8 = CRDT_JOIN_PAD_STORES == 2 ? 7u : 15u, m4 = CRDT_JOIN_PAD_STORES == 2 ? 15u : 31u;
+            // 1: to the end of the 64-byte sector; 2 (diagnostic): of the 128-byte line
+            constexpr uint32_t m8 = CRDT_JOIN_PAD_STORES == 2 ? 15u : 7u, m4 = CRDT_JOIN_PAD_STORES == 2 ? 31u : 15u;
             n8 = min(((obase + n_out + m8) & ~m8) - obase, lim);
             n4 = min(((obase + n_out + m4) & ~m4) - obase, lim);
             n8 = max(n8, n_out);

@@ -707,7 +707,7 @@ hipError_t launch_join_tiles(const BatchView& A, const BatchView& B, const OutVi
     hipLaunchKernelGGL((tile_scan_kernel<1024>), dim3(1), dim3(1024), 0, stream, A.n_docs, wk, tw);
     e = hipGetLastError();
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL((tile_split_kernel<256>), dim3(n_cu * 4), dim3(256), 0, stream, A, B, wk, tw);
+    hipLaunchKernelGGL((tile_split_kernel<256>), dim3(n_cu * tw.split_bpc), dim3(256), 0, stream, A, B, wk, tw);
     e = hipGetLastError();
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(tile_geo_kernel, dim3(n_cu * 4), dim3(256), 0, stream, A, B, tw);

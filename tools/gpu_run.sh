@@ -11,6 +11,7 @@
 #   prof     rocprofv3 kernel trace + stats of the bench (no CPU baseline) -> gpurun_out/prof_$TAG
 #   configs  bench + kernel trace per config in $CONFIGS
 #   pmc      PMC passes (tools/pmc.sh; one rocprofv3 --pmc run per counter group)
+#   pmcall   PMC passes for every config in $CONFIGS (default 2 3 4 5) -> gpurun_out/pmc_${TAG}_cN/
 #   probe    stamped fold probe (tools/fold_probe, built on the CPU side first)
 #   multi    the two-process device-summary test alone
 #   layout   HBM rate vs workgroup -> address mapping (tools/bw_layout)
@@ -48,6 +49,12 @@ for r in "$@"; do
       done ;;
     pmc)
       TAILN=10 step pmc_$TAG 1200 bash tools/pmc.sh ;;
+    pmcall)
+      # HEAD PMC of every config's dominant kernel (tools/pmc.sh; one rocprofv3 --pmc run per counter group)
+      for c in ${CONFIGS:-2 3 4 5}; do
+        CONFIG=$c TAG=${TAG}_c$c TAILN=12 step pmc_${TAG}_c$c 900 bash tools/pmc.sh
+        if ! grep -q "hbm_bytes_per_launch" gpurun_out/pmc_${TAG}_c$c.log; then echo "pmc c$c incomplete"; exit 1; fi
+      done ;;
     probe)
       TAILN=20 step probe_c3 120 tools/fold_probe 3
       TAILN=20 step probe_c5 120 tools/fold_probe 5 ;;
