@@ -35,7 +35,11 @@ pass fetch FETCH_SIZE
 pass write WRITE_SIZE
 pass sq SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU
 pass lds SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_SALU SQ_INSTS_SMEM SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS GRBM_GUI_ACTIVE GRBM_COUNT
-pass tcc TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum
+# L2 hits / misses and the memory-side request counts (compare boxes by counters); not fatal
+timeout -k 10 -s KILL 150 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum --output-format csv \
+  -d "$OUT/tcc" -o run -- $BENCH > "$OUT/tcc.log" 2>&1
+trc=$?; echo "[pmc tcc] rc=$trc"
+case $trc in 124|137|134|139) tail -5 "$OUT/tcc.log"; exit $trc ;; esac  # a kill or a fault ends the script
 if [ "${EXTRA:-0}" = 1 ]; then
   pass lds2 SQ_LDS_IDX_ACTIVE SQ_LDS_ADDR_CONFLICT SQ_LDS_UNALIGNED_STALL SQ_INSTS_VMEM SQ_INST_LEVEL_LDS SQ_ACCUM_PREV_HIRES
 fi
