@@ -238,7 +238,6 @@ class Config2:
         self.oab = OutBuffers(n, R, 2 * n * 64, device=dev)
         self.oba = OutBuffers(n, R, 2 * n * 64, device=dev, shared_keys=self._key_owner())
         self.ctx_ab = torch.zeros(R, dtype=torch.int64, device=dev)
-        self.ctx_ba = torch.zeros(R, dtype=torch.int64, device=dev)
         self.a, self.b = self.A.as_batch(), self.B.as_batch()
         self.merges_per_step = 2 * n
 
@@ -270,11 +269,14 @@ class Config2:
         return _outs(self.oab, self.oba)
 
     def post(self, s):
-        """Per-GPU causal-context summary of the outputs; returns the R-vector."""
+        """Per-GPU causal-context summary of the outputs; returns the R-vector.
+        Both merges of a pair end with the same clock, dstVV max srcVV
+        (awset.go:160, crdt-misc.go:43-55, written to both outputs by the
+        exchange), so the max over every output clock is the max over the A <- B
+        outputs' clocks: one summary pass, not two plus a max (the oracle parity
+        of both outputs' clocks: tests/test_gpu_parity.py)."""
         eng, n, R = self.eng, self.n, self.R
         eng.causal_context_async(self.oab.vv, n, R, self.ctx_ab, stream=s)
-        eng.causal_context_async(self.oba.vv, n, R, self.ctx_ba, stream=s)
-        eng.vv_max_async(self.ctx_ab, self.ctx_ba, R, stream=s)
         return self.ctx_ab
 
     def launches_per_step(self):
@@ -361,7 +363,6 @@ class Config4(Config2):
         self.oab = OutBuffers(n, R, 2 * self.total, device=dev)
         self.oba = OutBuffers(n, R, 2 * self.total, device=dev, shared_keys=self._key_owner())
         self.ctx_ab = torch.zeros(R, dtype=torch.int64, device=dev)
-        self.ctx_ba = torch.zeros(R, dtype=torch.int64, device=dev)
         self.a, self.b = self.A.as_batch(), self.B.as_batch()
         self.merges_per_step = 2 * n
         self.sizes = sizes
