@@ -93,12 +93,34 @@ __global__ __launch_bounds__(NT) void tile_scan_kernel(uint32_t n_docs, Work wk,
     }
 }
 
+// Merge-path split at diagonal k whose answer is known to lie in [lo, hi]
+// (merge_path searches the whole diagonal).
+__device__ __forceinline__ uint32_t merge_path_in(const uint64_t* dk, const uint64_t* sk, uint32_t k, uint32_t lo,
+                                                  uint32_t hi) {
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (dk[mid] <= sk[k - 1 - mid])
+            lo = mid + 1;
+        else
+            hi = mid;
+    }
+    return lo;
+}
+
+// kSplitRun consecutive tiles per thread: a tile after its document's previous
+// tile searches only the window its predecessor's split bounds (the split
+// moves by at most one tile along each array: i(t) <= i(t+1) <= i(t) + tile),
+// so the deep levels of the search -- a line fetched per level -- are fewer.
+constexpr uint32_t kSplitRun = 4;
+
 template <int NT>
 __global__ __launch_bounds__(NT) void tile_split_kernel(BatchView A, BatchView B, Work wk, TileWork tw) {
     const uint32_t total = *tw.total;
     const uint32_t total_slots = work_total(wk, A.n_docs);
     const uint32_t n_runs = (total_slots + kRun - 1) / kRun;
-    for (uint32_t g = blockIdx.x * NT + threadIdx.x; g < total; g += gridDim.x * NT) {
+    uint32_t pd = 0xFFFFFFFFu, pt = 0, pi = 0;  // this thread's previous tile: document, index, split
+    for (uint32_t g0 = (blockIdx.x * NT + threadIdx.x) * kSplitRun; g0 < total; g0 += gridDim.x * NT * kSplitRun)
+    for (uint32_t g = g0; g < min(g0 + kSplitRun, total); ++g) {
         // run: last r with run[r] <= g (run prefixes strictly increase: every slot has >= 1 tile)
         uint32_t lo = 0, hi = n_runs;
         while (hi - lo > 1) {
@@ -126,9 +148,17 @@ __global__ __launch_bounds__(NT) void tile_split_kernel(BatchView A, BatchView B
         if (d < A.n_docs) {
             const uint32_t nd = live_count(A.offsets, A.counts, d), ns = live_count(B.offsets, B.counts, d);
             const uint32_t k0 = min(t * tw.tile, nd + ns);
-            i0 = merge_path(A.keys + A.offsets[d], nd, B.keys + B.offsets[d], ns, k0);
+            uint32_t lo = k0 > ns ? k0 - ns : 0u, hi = k0 < nd ? k0 : nd;
+            if (d == pd && t == pt + 1u) {  // the previous tile's split bounds this one's
+                lo = max(lo, pi);
+                hi = min(hi, pi + tw.tile);
+            }
+            i0 = merge_path_in(A.keys + A.offsets[d], B.keys + B.offsets[d], k0, lo, hi);
             j0 = k0 - i0;
         }
+        pd = d;
+        pt = t;
+        pi = i0;
         tw.desc[g] = make_uint4(d, t, i0, j0);
         tw.flags[g] = 0ull;
     }
