@@ -123,6 +123,7 @@ struct crdt_ctx {
     uint32_t tile_shape = 9;                  // crdt_ctx_set_option("join_tile_shape")
     bool tile_nt_stores = true;               // crdt_ctx_set_option("join_tile_nt_stores")
     uint32_t tile_split_bpc = 4;              // crdt_ctx_set_option("join_tile_split_blocks_per_cu")
+    uint32_t tile_shards = 8;                 // crdt_ctx_set_option("join_tile_dispensers")
     size_t scratch_slots = 0;
     uint32_t max_doc_entries = 0xFFFFFFFFu;  // caller's promise (crdt_ctx_set_max_doc_entries)
     uint32_t join_docs_per_wave = 8;          // crdt_ctx_set_option("join_docs_per_wave")
@@ -356,6 +357,11 @@ int crdt_ctx_set_option(crdt_ctx* ctx, const char* name, int64_t value) {
         ctx->tile_shape = (uint32_t)value;
         return CRDT_OK;
     }
+    if (!strcmp(name, "join_tile_dispensers")) {  // tile dispenser words: 1, or 8 (one per XCD, tile.hip)
+        if (value != 1 && value != 8) return CRDT_E_INVALID;
+        ctx->tile_shards = (uint32_t)value;
+        return CRDT_OK;
+    }
     if (!strcmp(name, "join_tile_split_blocks_per_cu")) {  // grid of the tile plan's merge-path search
         if (value < 1 || value > 64) return CRDT_E_INVALID;
         ctx->tile_split_bpc = (uint32_t)value;
@@ -450,9 +456,9 @@ static int join_common(crdt_ctx* ctx, const crdt_awset_batch* dst, const crdt_aw
         if (rc != CRDT_OK) return rc;
         uint32_t* w = ctx->ws.as<uint32_t>(0);
         tw = TileWork{ctx->tile_desc.as<uint4>(), ctx->tile_geo.as<uint4>(), ctx->tile_flags.as<uint64_t>(), ctx->tile_slot.as<uint32_t>(),
-                      ctx->tile_run.as<uint32_t>(), w + 3, w + 4, w + 5, ctx->tile_cap,
+                      ctx->tile_run.as<uint32_t>(), w + 3, w + 8, w + 5, ctx->tile_cap,
                       tile_positions(ctx->tile_shape), ctx->tile_shape, ctx->tile_nt_stores ? 1u : 0u,
-                      ctx->tile_split_bpc};
+                      ctx->tile_split_bpc, ctx->tile_shards};
     }
     // the per-call counters are read only by the large-document paths
     if (!no_large && launch_reset_work(ctx->ws.as<uint32_t>(0), s) != hipSuccess) return CRDT_E_HIP;

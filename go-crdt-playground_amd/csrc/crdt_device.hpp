@@ -71,7 +71,7 @@ struct Work {
     uint32_t* wl_count;    // number of docs pushed to the block-path worklist
     uint32_t* wl_head;     // dequeue head of the block path
     uint32_t* worklist;    // [n_docs]
-    uint32_t* chunk_ctr;   // [8] chunk dispenser shards of the wave path
+    uint32_t* chunk_ctr;   // [8] dispenser shards (the tile path's, TileWork::head)
     uint32_t* defer;       // [n_docs] folds: documents the lean pass leaves to the general one
     uint32_t* defer_count; // number of deferred documents
 };
@@ -109,13 +109,14 @@ struct TileWork {
     uint32_t* slot_incl;  // [n_docs] inclusive tile count within the slot's run
     uint32_t* run;        // [ceil(n_docs/kRun)] run sums -> exclusive prefixes
     uint32_t* total;      // workspace word: tiles of this call
-    uint32_t* head;       // workspace word: tile dispenser
+    uint32_t* head;       // workspace words [shards]: tile dispensers (tile.hip, tile_take)
     uint32_t* fallback;   // workspace word: 1 = tiles exceed cap, block kernel runs
     uint32_t cap;
     uint32_t tile;   // merged positions per tile (= the tile kernel's NT * IPT)
     uint32_t shape;  // tile kernel shape (tile.hip, tile_positions)
     uint32_t nt_stores;  // non-temporal output stores ("join_tile_nt_stores")
     uint32_t split_bpc;  // tile_split_kernel workgroups per CU ("join_tile_split_blocks_per_cu")
+    uint32_t shards;     // tile dispenser words, 1 or 8 ("join_tile_dispensers")
 };
 
 // ---- slab order of a grid's blocks.  A streaming kernel whose concurrently

@@ -178,6 +178,23 @@ struct TileSmem {
     uint64_t prev_key;
 };
 
+// The tile dispenser, sharded: workgroup b takes the tiles s, s + S, s + 2S, ...
+// (s = b mod S, S = tw.shards) in order from head word s.  One word taken by
+// every workgroup saturates near 88 M takes/s (MI355X_MICROARCH.md, 'dequeue')
+// -- config 4 takes 1.1 M tiles per launch -- while S = 8 words, one per XCD
+// (workgroups are dispatched to the XCDs round-robin, so b mod 8 is the XCD),
+// spread the takes.  Progress: a taken tile is published without waiting; a
+// look-back waits only on smaller tiles, and the smallest tile not yet
+// published is either held by a workgroup whose pending look-back concerns
+// smaller, published tiles only, or not taken yet, in which case the resident
+// workgroups of its shard (blocks 0..S-1 start first) are not held by it
+// either and reach it.  Needs S resident workgroups, as the persistent grid
+// (the occupancy query) always has.
+__device__ __forceinline__ uint32_t tile_take(const TileWork& tw) {
+    const uint32_t S = tw.shards, s = blockIdx.x % S;
+    return atomicAdd(tw.head + s, 1u) * S + s;
+}
+
 __device__ __forceinline__ uint64_t flag_load(const uint64_t* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -501,7 +518,7 @@ __global__ __launch_bounds__(NT) void join_tile_kernel(BatchView A, BatchView B,
     TileRegs<IPT> rg;
     STAMP_DECL
 
-    if (tid == 0) sm.word[0] = atomicAdd(tw.head, 1u);
+    if (tid == 0) sm.word[0] = tile_take(tw);
     __syncthreads();
     uint32_t g = sm.word[0];
     TileGeo x{};
@@ -531,7 +548,7 @@ __global__ __launch_bounds__(NT) void join_tile_kernel(BatchView A, BatchView B,
             // next tile now (a tile taken earlier would be held while this one's
             // look-back waits, and its successors would wait on that in turn)
             if (lane == 0) {
-                sm.word[0] = atomicAdd(tw.head, 1u);
+                sm.word[0] = tile_take(tw);
                 sm.word[1] = prefix;
             }
         }
@@ -576,7 +593,7 @@ __global__ __launch_bounds__(NT) void join_tile_pipe_kernel(BatchView A, BatchVi
     TileRegs<IPT> rg;
     STAMP_DECL
 
-    if (tid == 0) word[0] = atomicAdd(tw.head, 1u);
+    if (tid == 0) word[0] = tile_take(tw);
     __syncthreads();
     uint32_t g1 = word[0];
     if (g1 >= total) return;
@@ -603,7 +620,7 @@ __global__ __launch_bounds__(NT) void join_tile_pipe_kernel(BatchView A, BatchVi
             }
             if (lane == 0) {
                 word[1] = p0;
-                word[0] = atomicAdd(tw.head, 1u);
+                word[0] = tile_take(tw);
             }
         }
         __syncthreads();

@@ -160,6 +160,11 @@ def test_tile_fallback_and_switch(eng):
     try:
         eng.set_option("join_tile_capacity", 3)
         assert_same(eng.join(dst, src), want, dst.n_docs, R)
+        rc, want2 = oracle.join(src, dst)
+        assert rc == 0
+        o1, o2 = eng.exchange(dst, src)  # both block-kernel passes (their own dequeue heads)
+        assert_same(o1, want, dst.n_docs, R)
+        assert_same(o2, want2, dst.n_docs, R)
         eng.set_option("join_tile_capacity", 1 << 20)
         eng.set_option("join_tiles", 0)
         assert_same(eng.join(dst, src), want, dst.n_docs, R)
@@ -167,6 +172,23 @@ def test_tile_fallback_and_switch(eng):
         eng.set_option("join_tiles", 1)
         eng.set_option("join_tile_capacity", 1 << 20)
     assert_same(eng.join(dst, src), want, dst.n_docs, R)
+
+
+@pytest.mark.parametrize("dispensers", [1, 8])
+def test_tile_dispensers(eng, dispensers):
+    """The tile dispenser as one word or sharded over eight (tile.hip,
+    tile_take): the same bits, on documents of many tiles next to small ones."""
+    rng = random.Random(9)
+    R = 3
+    sz = lambda: rng.choice([5, 64, 300, 2047, 2049, 9000, 40000])  # noqa: E731
+    dsts = [random_state(rng, R, sz(), 90000, 30) for _ in range(48)]
+    srcs = [random_state(rng, R, sz(), 90000, 30) for _ in range(48)]
+    dst, src = batch_of(R, dsts), batch_of(R, srcs)
+    try:
+        eng.set_option("join_tile_dispensers", dispensers)
+        check_join_and_exchange(eng, dst, src, R)
+    finally:
+        eng.set_option("join_tile_dispensers", 8)
 
 
 def _sub(h, d0, d1, R):

@@ -30,13 +30,15 @@ def main():
     o1, o2 = OutBuffers(n, 2, 2 * total, device=dev), OutBuffers(n, 2, 2 * total, device=dev)
     a, b = A.as_batch(), B.as_batch()
     ref = None
-    # shape:nt_stores[:split workgroups per CU]
-    shapes = [tuple(int(v) for v in (a + ":4").split(":")[:3]) for a in sys.argv[2:]] or \
-        [(2, 1, 4), (4, 1, 4), (4, 0, 4), (5, 1, 4), (6, 1, 4), (7, 1, 4), (1, 1, 4), (4, 1, 4), (2, 1, 4)]
-    for shape, nts, sbpc in shapes:
+    # shape:nt_stores[:split workgroups per CU[:dispenser words]]
+    dflt = (9, 1, 4, 8)
+    shapes = [tuple([int(v) for v in a.split(":")] + list(dflt[len(a.split(":")):])) for a in sys.argv[2:]] or \
+        [(9, 1, 4, 8), (9, 1, 4, 1)]
+    for shape, nts, sbpc, shards in shapes:
         eng.set_option("join_tile_shape", shape)
         eng.set_option("join_tile_nt_stores", nts)
         eng.set_option("join_tile_split_blocks_per_cu", sbpc)
+        eng.set_option("join_tile_dispensers", shards)
         eng.exchange_async(a, b, o1, o2)
         eng.sync()
         got = (o1.counts.clone(), o1.keys.clone(), o1.actors.clone(), o1.counters.clone(), o2.counts.clone(),
@@ -50,8 +52,8 @@ def main():
             eng.exchange_async(a, b, o1, o2)
         ev[1].record()
         eng.sync()
-        print("shape %d nt %d split_bpc %d: %.3f ms per exchange call (same output: %s)" % (
-            shape, nts, sbpc, ev[0].elapsed_time(ev[1]) / 5, same), flush=True)
+        print("shape %d nt %d split_bpc %d dispensers %d: %.3f ms per exchange call (same output: %s)" % (
+            shape, nts, sbpc, shards, ev[0].elapsed_time(ev[1]) / 5, same), flush=True)
     eng.close()
 
 
