@@ -352,8 +352,8 @@ int crdt_ctx_set_option(crdt_ctx* ctx, const char* name, int64_t value) {
     }
     if (!strcmp(name, "join_tile_shape")) {  // threads x positions: look-back per tile 0: 512x4, 1: 256x4, 2: 256x8,
                                              // 3: 1024x2; deferred by a tile 4: 256x4, 5: 512x2, 6: 256x8, 7: 128x8,
-                                             // and aligned store windows 8: 256x4, 9: 512x2 (default)
-        if (value < 0 || value > 9) return CRDT_E_INVALID;
+                                             // and aligned store windows 8: 256x4, 9: 512x2 (default), 10: 256x2
+        if (value < 0 || value > 10) return CRDT_E_INVALID;
         ctx->tile_shape = (uint32_t)value;
         return CRDT_OK;
     }

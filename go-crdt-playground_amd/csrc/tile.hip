@@ -739,6 +739,7 @@ uint32_t tile_positions(uint32_t shape) {
         case 7: return 128 * 8;
         case 8: return 256 * 4;  // aligned store windows
         case 9: return 512 * 2;
+        case 10: return 256 * 2;  // aligned store windows, half tiles (six workgroups per CU by LDS)
         default: return 512 * 4;
     }
 }
@@ -770,6 +771,7 @@ hipError_t launch_join_tiles(const BatchView& A, const BatchView& B, const OutVi
         case 7: return launch_tile_pipe<128, 8>(A, B, o1, o2, wk, tw, n_cu, stream);
         case 8: return launch_tile_pipe<256, 4, true>(A, B, o1, o2, wk, tw, n_cu, stream);
         case 9: return launch_tile_pipe<512, 2, true>(A, B, o1, o2, wk, tw, n_cu, stream);
+        case 10: return launch_tile_pipe<256, 2, true>(A, B, o1, o2, wk, tw, n_cu, stream);
         default: return launch_tile_kernel<512, 4>(A, B, o1, o2, wk, tw, n_cu, stream);
     }
 }
