@@ -118,7 +118,9 @@ struct crdt_ctx {
     // tile_cap tiles, per-slot and per-run tile counts for the worklist
     DevBuf tile_desc, tile_geo, tile_flags, tile_slot, tile_run;
     DevBuf sort_tmp, sort_idx, sort_ends;  // ingest sort (sort.hip)
-    uint32_t tile_cap = 1u << 20;             // crdt_ctx_set_option("join_tile_capacity")
+    // crdt_ctx_set_option("join_tile_capacity"): 2^22 tiles (235 MB of tile workspace, on
+    // first use); config 4 needs 1.035 M tiles of 1,024 positions, 2.07 M of 512
+    uint32_t tile_cap = 1u << 22;
     bool join_tiles = true;                   // crdt_ctx_set_option("join_tiles")
     uint32_t tile_shape = 9;                  // crdt_ctx_set_option("join_tile_shape")
     bool tile_nt_stores = true;               // crdt_ctx_set_option("join_tile_nt_stores")

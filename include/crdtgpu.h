@@ -163,7 +163,12 @@ int crdt_ctx_set_max_doc_entries(crdt_ctx* ctx, uint32_t max_entries);
  *   "join_slab_blocks_per_cu" 0..64   wave kernel block order: slabs of G = this x CUs
  *                                     blocks (crdt_device.hpp SlabMap; 0 = in order)
  *   "fold_lean_first"     0|1         folds: slot-walk pass first, the rest deferred (default 1)
- *   (also "join_tile_capacity", "join_tile_shape", "join_tile_nt_stores",
+ *   "join_tile_capacity"  1..2^28     large documents: merge-path tiles of 1,024 merged
+ *                                     positions the workspace holds (default 2^22, 56 B
+ *                                     each, allocated on first use); a call needing more
+ *                                     takes the per-document block kernel instead
+ *   "join_tile_dispensers" 1|8        tile dispenser words (default 8, one per XCD)
+ *   (also "join_tile_shape", "join_tile_nt_stores", "join_tile_split_blocks_per_cu",
  *   "join_tiles": see api.cpp)
  * and one layout option of the host-buffer (*_batch) joins, exchanges and folds:
  *   "pack_batch_outputs"  0|1         1: out holds only the live entries, doc d

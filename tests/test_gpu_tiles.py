@@ -165,12 +165,12 @@ def test_tile_fallback_and_switch(eng):
         o1, o2 = eng.exchange(dst, src)  # both block-kernel passes (their own dequeue heads)
         assert_same(o1, want, dst.n_docs, R)
         assert_same(o2, want2, dst.n_docs, R)
-        eng.set_option("join_tile_capacity", 1 << 20)
+        eng.set_option("join_tile_capacity", 1 << 22)
         eng.set_option("join_tiles", 0)
         assert_same(eng.join(dst, src), want, dst.n_docs, R)
     finally:
         eng.set_option("join_tiles", 1)
-        eng.set_option("join_tile_capacity", 1 << 20)
+        eng.set_option("join_tile_capacity", 1 << 22)
     assert_same(eng.join(dst, src), want, dst.n_docs, R)
 
 

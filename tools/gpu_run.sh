@@ -99,6 +99,8 @@ for r in "$@"; do
         --output-format csv -d gpurun_out/btrace_$TAG -o run -- go-crdt-playground_amd/host/build/boundary_bench 65536 ;;
     tsweep)
       TAILN=12 step tsweep_$TAG 400 python3 tools/tile_sweep.py 16384 ${TSHAPES:-9:1 10:1 9:1 10:1 9:1 10:1} ;;
+    tprobe)
+      for sh in ${TPROBE:-9}; do TAILN=14 step tprobe_${sh}_$TAG 200 python3 tools/tile_probe.py $sh; done ;;
     xab)
       TAILN=12 step xab_$TAG 400 python3 tools/exchange_ab.py ;;
     ptest)

@@ -30,6 +30,7 @@ def main():
     o1, o2 = OutBuffers(n, 2, 2 * total, device=dev), OutBuffers(n, 2, 2 * total, device=dev)
     a, b = A.as_batch(), B.as_batch()
     ref = None
+    eng.set_option("join_tile_capacity", 1 << 22)  # room for the smaller tile shapes (2.07 M tiles of 512)
     # shape:nt_stores[:split workgroups per CU[:dispenser words]]
     dflt = (9, 1, 4, 8)
     shapes = [tuple([int(v) for v in a.split(":")] + list(dflt[len(a.split(":")):])) for a in sys.argv[2:]] or \
