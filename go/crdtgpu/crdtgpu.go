@@ -284,6 +284,7 @@ func (e *Engine) Merge(dst, src *crdt.AWSet) error {
 }
 
 // MergeBatch does dsts[i].Merge(srcs[i]) for every i in one call
+// (same logic as host/crdt.hpp MergeBatch, tested on the GPU by tests/cpp/test_scenarios.cpp)
 // (crdt_awset_join_batch). Destinations must be distinct. Every merge reads
 // the states as they were when the call began (a source that is also a
 // destination of the batch is read before it changes).
@@ -328,6 +329,8 @@ func (e *Engine) MergeBatch(dsts, srcs []*crdt.AWSet) error {
 }
 
 // ExchangeBatch is anti-entropy both ways in one call
+// (same logic as host/crdt.hpp ExchangeBatch, tested on the GPU by tests/cpp/test_scenarios.cpp
+// and timed by tests/cpp/boundary_bench.cpp)
 // (crdt_awset_exchange_batch): for every i, as[i] becomes
 // as[i].Clone().Merge(bs[i]) and bs[i] becomes bs[i].Clone().Merge(as[i]), the
 // two merges of ONE snapshot, from one read of the pair. This is not the
@@ -383,6 +386,7 @@ func (e *Engine) ExchangeBatch(as, bs []*crdt.AWSet) error {
 // ---------------------------------------------------------------- ordered folds
 
 // FoldBatch does, for every i, dsts[i].Merge(s) for s in srcs[i] in order
+// (same logic as host/crdt.hpp FoldBatch, tested on the GPU by tests/cpp/test_scenarios.cpp)
 // (AWSet semantics, awset.go:103-161) in one call (crdt_awset_fold_batch).
 func (e *Engine) FoldBatch(dsts []*crdt.AWSet, srcs [][]*crdt.AWSet) error {
 	ds := make([]docState, len(dsts))
@@ -403,6 +407,8 @@ func (e *Engine) DeltaMerge(dst, src *AWSetDelta) error {
 	return e.DeltaMergeBatch([]*AWSetDelta{dst}, [][]*AWSetDelta{{src}})
 }
 
+// (DeltaMergeBatch: same logic as host/crdt.hpp DeltaMergeBatch, tested on the GPU by
+// tests/cpp/test_scenarios.cpp.)
 // DeltaMergeBatch does, for every i, dsts[i].Merge(s) for s in srcs[i] in
 // order (AWSetDelta semantics, awset-delta_test.go:51-166: the path select on
 // Counter(src.Actor), MakeDeltaMergeData's pruning, the no-op that skips even
