@@ -718,7 +718,12 @@ int crdt_host_alloc(size_t bytes, void** out) {
     if (!out) return CRDT_E_INVALID;
     *out = nullptr;
     if (bytes == 0) bytes = 1;
-    return hipHostMalloc(out, bytes, hipHostMallocDefault) == hipSuccess ? CRDT_OK : CRDT_E_NOMEM;
+    // CRDT_HOST_MALLOC_FLAGS (diagnostics): hipHostMalloc flags instead of the default
+    static const unsigned flags = [] {
+        const char* e = std::getenv("CRDT_HOST_MALLOC_FLAGS");
+        return e ? (unsigned)std::strtoul(e, nullptr, 0) : (unsigned)hipHostMallocDefault;
+    }();
+    return hipHostMalloc(out, bytes, flags) == hipSuccess ? CRDT_OK : CRDT_E_NOMEM;
 }
 
 void crdt_host_free(void* p) {

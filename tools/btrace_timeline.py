@@ -40,6 +40,9 @@ def main():
     gpu += [(ms(r["Start_Timestamp"]), ms(r["End_Timestamp"]), "kernel " + r["Kernel_Name"].split("(")[0][:48])
             for r in kt]
     gpu.sort()
+    own = {}  # correlation id -> the GPU op the call submitted
+    for r in cp + kt:
+        own[r["Correlation_Id"]] = (ms(r["Start_Timestamp"]), ms(r["End_Timestamp"]))
     calls = sorted(api, key=lambda r: int(r["Start_Timestamp"]))
     main_tid = max(set(r["Thread_Id"] for r in calls), key=lambda t: sum(1 for r in calls if r["Thread_Id"] == t))
     busy_total = 0.0
@@ -52,9 +55,11 @@ def main():
         during = [(s, e, w) for s, e, w in gpu if e > a and s < b]
         busy = sum(min(e, b) - max(s, a) for s, e, _ in during)
         busy_total += b - a
-        print("%10.3f %8.3f ms  %-28s gpu busy %5.1f%% of it; %s" % (
-            a, b - a, r["Function"][:28], 100.0 * busy / (b - a) if b > a else 0.0,
-            "; ".join("%s [%.3f-%.3f]" % (w, s, e) for s, e, w in during[:4])))
+        mine = own.get(r["Correlation_Id"])
+        print("%10.3f %8.3f ms  %-22s gpu busy %5.1f%% of it;%s %s" % (
+            a, b - a, r["Function"][:22], 100.0 * busy / (b - a) if b > a else 0.0,
+            (" its own op starts %+.3f ms after the call returns;" % (mine[0] - b)) if mine else "",
+            "; ".join("%s [%.3f-%.3f]" % (w, s, e) for s, e, w in during[:3])))
     print("calls >= %.2f ms on the main thread: %.1f ms in total" % (thr, busy_total))
 
 
