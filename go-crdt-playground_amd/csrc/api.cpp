@@ -8,6 +8,8 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
+#include <mutex>
 #include <new>
 #include <vector>
 
@@ -101,6 +103,27 @@ struct DevBuf {
         return reinterpret_cast<T*>(static_cast<char*>(p) + byte_off);
     }
 };
+
+// The page-locked blocks crdt_host_alloc made (base -> size): a *_batch call
+// whose input arrays all lie in one of them is staged by ONE copy of the span
+// they cover (Stager), because each runtime H2D copy call costs the host 1-7
+// ms before its DMA is even submitted, whatever its size
+// (profiles/r05i_boundary_timeline.txt), while the span moves at PCIe rate.
+std::mutex g_host_mu;
+std::map<uintptr_t, size_t> g_host_blocks;
+
+bool host_block(const void* p, uintptr_t& base, size_t& size) {
+    const uintptr_t a = (uintptr_t)p;
+    std::lock_guard<std::mutex> lk(g_host_mu);
+    auto it = g_host_blocks.upper_bound(a);
+    if (it == g_host_blocks.begin()) return false;
+    --it;
+    if (a >= it->first + it->second) return false;
+    base = it->first;
+    size = it->second;
+    return true;
+}
+
 
 }  // namespace
 
@@ -723,11 +746,20 @@ int crdt_host_alloc(size_t bytes, void** out) {
         const char* e = std::getenv("CRDT_HOST_MALLOC_FLAGS");
         return e ? (unsigned)std::strtoul(e, nullptr, 0) : (unsigned)hipHostMallocDefault;
     }();
-    return hipHostMalloc(out, bytes, flags) == hipSuccess ? CRDT_OK : CRDT_E_NOMEM;
+    if (hipHostMalloc(out, bytes, flags) != hipSuccess) return CRDT_E_NOMEM;
+    std::lock_guard<std::mutex> lk(g_host_mu);
+    g_host_blocks[(uintptr_t)*out] = bytes;
+    return CRDT_OK;
 }
 
 void crdt_host_free(void* p) {
-    if (p) (void)hipHostFree(p);
+    if (p) {
+        {
+            std::lock_guard<std::mutex> lk(g_host_mu);
+            g_host_blocks.erase((uintptr_t)p);
+        }
+        (void)hipHostFree(p);
+    }
 }
 
 int crdt_clock_probe(crdt_ctx* ctx, double* mhz) {
@@ -839,14 +871,53 @@ struct PhaseClock {
     }
 };
 
+constexpr int kSpanSlot = 31;  // ctx->stage[kSpanSlot]: the device image of a host block's span
+
 struct Stager {
     crdt_ctx* ctx;
     int next = 0;
     int rc = CRDT_OK;
+    // the host block of this call's first staged array (span staging), the
+    // device image of that whole block, and the part of it to copy
+    uintptr_t blk = 0;
+    size_t blk_size = 0;
+    char* dimg = nullptr;
+    size_t lo = SIZE_MAX, hi = 0;
+    bool flushed = false;
     template <typename T>
     T* put(const T* host, size_t n) {  // allocate + copy in (n elements)
         if (rc != CRDT_OK) return nullptr;
         static const bool trace = std::getenv("CRDT_TRACE_STAGE") != nullptr;  // diagnostics: host time per step
+        static const bool span = std::getenv("CRDT_NO_SPAN_STAGING") == nullptr;
+        if (span && host && n) {
+            if (!blk) {
+                uintptr_t b0 = 0;
+                size_t sz = 0;
+                if (host_block(host, b0, sz) && sz <= ((size_t)4 << 30)) {  // (a larger block: array by array)
+                    rc = ctx->stage[kSpanSlot].reserve(sz);
+                    if (rc != CRDT_OK) return nullptr;
+                    blk = b0;
+                    blk_size = sz;
+                    dimg = ctx->stage[kSpanSlot].as<char>();
+                }
+            }
+            const uintptr_t a = (uintptr_t)host, bytes = n * sizeof(T);
+            if (blk && a >= blk && a + bytes <= blk + blk_size) {
+                const size_t off = a - blk;
+                if (flushed) {  // staged after the span went: its own copy, into the same image
+                    if (hipMemcpyAsync(dimg + off, host, bytes, hipMemcpyHostToDevice, ctx->stream) != hipSuccess)
+                        rc = CRDT_E_HIP;
+                } else {
+                    lo = std::min(lo, off);
+                    hi = std::max(hi, off + (size_t)bytes);
+                }
+                return reinterpret_cast<T*>(dimg + off);
+            }
+        }
+        if (next >= kSpanSlot) {
+            rc = CRDT_E_INVALID;
+            return nullptr;
+        }
         const auto t0 = std::chrono::steady_clock::now();
         DevBuf& b = ctx->stage[next++];
         rc = b.reserve(std::max<size_t>(n, 1) * sizeof(T));
@@ -865,6 +936,18 @@ struct Stager {
     template <typename T>
     T* room(size_t n) {
         return put<T>(nullptr, n);
+    }
+    // Copy the span of the host block that this call's arrays cover (one call).
+    void flush() {
+        if (rc != CRDT_OK || flushed || !blk || hi <= lo) {
+            flushed = blk != 0;
+            return;
+        }
+        const size_t a = lo & ~(size_t)255;  // (the image keeps the block's alignment)
+        if (hipMemcpyAsync(dimg + a, reinterpret_cast<const char*>(blk) + a, hi - a, hipMemcpyHostToDevice,
+                           ctx->stream) != hipSuccess)
+            rc = CRDT_E_HIP;
+        flushed = true;
     }
 };
 
@@ -944,6 +1027,7 @@ int fetch_merge_out(crdt_ctx* ctx, Stager& st, const crdt_awset_out* h, const cr
     const uint32_t* poff = st.put(h->offsets, (size_t)n + 1);
     const crdt_awset_out p{nullptr, nullptr, st.room<uint64_t>(tot), st.room<uint32_t>(tot), st.room<uint64_t>(tot),
                            nullptr};
+    st.flush();  // the inputs' span, if they lie in one crdt_host_alloc block
     if (st.rc != CRDT_OK) return st.rc;
     rc = hip_err(launch_pack_out(view(&d), poff, n, view(&p), (uint32_t)ctx->n_cu, ctx->stream));
     if (rc == CRDT_OK && keys) rc = get(h->keys, p.keys, tot, ctx->stream);
@@ -966,6 +1050,7 @@ int crdt_awset_sort_batch(crdt_ctx* ctx, const crdt_awset_batch* in, const crdt_
     Stager st{ctx};
     crdt_awset_batch di = stage_batch(st, in);
     crdt_awset_out dout = stage_out(st, n, in->R, slots);
+    st.flush();  // the inputs' span, if they lie in one crdt_host_alloc block
     if (st.rc != CRDT_OK) return st.rc;
     rc = crdt_awset_sort_async(ctx, &di, (uint32_t)slots, &dout, ctx->stream);
     if (rc == CRDT_OK) rc = fetch_out(out, dout, n, in->R, slots, ctx->stream);
@@ -1011,6 +1096,7 @@ int crdt_awset_apply_batch(crdt_ctx* ctx, const crdt_awset_batch* state, const c
         dto.actors = st.room<uint32_t>(tin + nops);
         dto.counters = st.room<uint64_t>(tin + nops);
     }
+    st.flush();  // the inputs' span, if they lie in one crdt_host_alloc block
     if (st.rc != CRDT_OK) return st.rc;
     rc = crdt_awset_apply_async(ctx, &ds, tombs ? &dt : nullptr, &dops, &dout, tomb_out ? &dto : nullptr,
                                 ctx->stream);
@@ -1039,6 +1125,7 @@ int crdt_awset_join_batch(crdt_ctx* ctx, const crdt_awset_batch* dst, const crdt
     crdt_awset_batch dd = stage_batch(st, dst), ds = stage_batch(st, src);
     const size_t slots = (size_t)dst->offsets[dst->n_docs] + src->offsets[src->n_docs];
     crdt_awset_out dout = stage_out(st, dst->n_docs, dst->R, slots);
+    st.flush();  // the inputs' span, if they lie in one crdt_host_alloc block
     if (st.rc != CRDT_OK) return st.rc;
     rc = check_order(ctx, dd.offsets, dd.counts, dd.n_docs, dd.keys);
     if (rc == CRDT_OK) rc = check_order(ctx, ds.offsets, ds.counts, ds.n_docs, ds.keys);
@@ -1064,6 +1151,7 @@ int crdt_awset_exchange_batch(crdt_ctx* ctx, const crdt_awset_batch* a, const cr
     const size_t slots = (size_t)a->offsets[a->n_docs] + b->offsets[b->n_docs];
     crdt_awset_out o1 = stage_out(st, a->n_docs, a->R, slots);
     crdt_awset_out o2 = stage_out(st, a->n_docs, a->R, slots);
+    st.flush();  // the inputs' span, if they lie in one crdt_host_alloc block
     if (st.rc != CRDT_OK) return st.rc;
     // host outputs sharing one key column: one device column, written and fetched once
     const bool share = out_ab->keys == out_ba->keys;
@@ -1115,6 +1203,7 @@ int crdt_awset_fold_batch(crdt_ctx* ctx, int mode, const crdt_awset_batch* dst, 
         ds.tcounters = st.put(srcs->tcounters, nt);
     }
     crdt_awset_out dout = stage_out(st, dst->n_docs, dst->R, total);
+    st.flush();  // the inputs' span, if they lie in one crdt_host_alloc block
     if (st.rc != CRDT_OK) return st.rc;
     rc = check_order(ctx, dd.offsets, dd.counts, dd.n_docs, dd.keys);
     if (rc == CRDT_OK) rc = check_order(ctx, ds.entry_off, nullptr, ns, ds.keys);

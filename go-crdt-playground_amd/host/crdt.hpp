@@ -160,7 +160,24 @@ class Engine {
     }
     template <typename T>
     T* pinned(int role, size_t n) {
+        if (carved_[role] && n * sizeof(T) <= carved_n_[role]) return static_cast<T*>(carved_[role]);
         return static_cast<T*>(pin_[role].get(n * sizeof(T)));
+    }
+    // Place the given roles' arrays in ONE page-locked block (256-byte aligned
+    // sub-arrays): the C ABI stages arrays that lie in one crdt_host_alloc
+    // block with a single copy (api.cpp, Stager::flush) instead of one runtime
+    // copy call each.  Replaces the previous call's carving.
+    void carve(std::initializer_list<std::pair<int, size_t>> roles) {
+        for (auto& c : carved_) c = nullptr;
+        size_t total = 0;
+        for (const auto& r : roles) total += (r.second + 255) & ~(size_t)255;
+        char* base = static_cast<char*>(arena_.get(total));
+        size_t off = 0;
+        for (const auto& r : roles) {
+            carved_[r.first] = base + off;
+            carved_n_[r.first] = r.second;
+            off += (r.second + 255) & ~(size_t)255;
+        }
     }
     // host arrays of map iterators per slot (0: destinations, 1: sources),
     // grown on demand and reused: no per-call allocation or first touch
@@ -174,6 +191,9 @@ class Engine {
    private:
     crdt_ctx* ctx_ = nullptr;
     detail::PinnedBuf pin_[detail::kPinSlots];
+    detail::PinnedBuf arena_;  // the carved input block
+    void* carved_[detail::kPinSlots] = {};
+    size_t carved_n_[detail::kPinSlots] = {};
     std::vector<Entries::iterator> its_[2];
     detail::Batch* batch_ = nullptr;
 };
@@ -821,6 +841,11 @@ inline crdt_awset_batch pack(Batch& b, Engine& e, bool tombs) {
     layout(b, tombs);
     const size_t n = b.n_docs, ns = b.src.size(), R = b.R;
     const size_t nd = b.dfirst[n], nse = b.sfirst[ns], nt = b.tfirst[ns];
+    // every input array of the call in one page-locked block: staged by one copy
+    e.carve({{kD_OFF, (n + 1) * 4}, {kS_OFF, (ns + 1) * 4}, {kD_KEY, nd * 8}, {kD_ACT, nd * 4}, {kD_CTR, nd * 8},
+             {kD_VV, n * R * 8}, {kS_KEY, nse * 8}, {kS_ACT, nse * 4}, {kS_CTR, nse * 8}, {kS_VV, ns * R * 8},
+             {kS_TKEY, (tombs ? nt : 0) * 8}, {kS_TACT, (tombs ? nt : 0) * 4}, {kS_TCTR, (tombs ? nt : 0) * 8},
+             {kS_DOC, (n + 1) * 4}, {kS_SACT, ns * 4}, {kS_TOFF, (ns + 1) * 4}});
     uint32_t* doff = e.pinned<uint32_t>(kD_OFF, n + 1);
     std::copy(b.dfirst.begin(), b.dfirst.end(), doff);
     uint32_t* soff = e.pinned<uint32_t>(kS_OFF, ns + 1);

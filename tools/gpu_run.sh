@@ -93,6 +93,12 @@ for r in "$@"; do
       TAILN=40 step bmalloc_keep_$TAG 200 env CRDT_TRACE_STAGE=1 MALLOC_TRIM_THRESHOLD_=68719476736 MALLOC_MMAP_THRESHOLD_=33554432 MALLOC_TOP_PAD_=1073741824 go-crdt-playground_amd/host/build/boundary_bench 65536
       TAILN=2 step bmalloc_keep2_$TAG 200 env MALLOC_TRIM_THRESHOLD_=68719476736 MALLOC_MMAP_THRESHOLD_=33554432 MALLOC_TOP_PAD_=1073741824 go-crdt-playground_amd/host/build/boundary_bench 65536
       TAILN=2 step bmalloc_default2_$TAG 200 env go-crdt-playground_amd/host/build/boundary_bench 65536 ;;
+    bspan)
+      # the mirror's inputs in one page-locked block, staged by one copy (default) vs one copy per array
+      for v in "span:" "perarray:CRDT_NO_SPAN_STAGING=1" "span2:" "perarray2:CRDT_NO_SPAN_STAGING=1"; do
+        n=${v%%:*}; e=${v#*:}
+        TAILN=12 step bspan_${n}_$TAG 200 env CRDT_TRACE_STAGE=1 $e go-crdt-playground_amd/host/build/boundary_bench 65536
+      done ;;
     bcoh)
       # is each H2D staging copy's host-side delay the runtime keeping non-coherent page-locked memory coherent?
       for v in "default:" "hipcoh:HIP_HOST_COHERENT=1" "coherent:CRDT_HOST_MALLOC_FLAGS=0x40000000" "noncoh:CRDT_HOST_MALLOC_FLAGS=0x80000000" "default2:"; do
