@@ -474,7 +474,7 @@ static int join_common(crdt_ctx* ctx, const crdt_awset_batch* dst, const crdt_aw
     if (tiles) {
         const size_t n = std::max<size_t>(dst->n_docs, 1);
         rc = grow(ctx->tile_desc, (size_t)ctx->tile_cap * 16, cap);
-        if (rc == CRDT_OK) rc = grow(ctx->tile_geo, (size_t)ctx->tile_cap * 32, cap);
+        if (rc == CRDT_OK) rc = grow(ctx->tile_geo, ((size_t)ctx->tile_cap + 8) * 32, cap);  // (+8: geo_slot)
         if (rc == CRDT_OK) rc = grow(ctx->tile_flags, (size_t)ctx->tile_cap * 8, cap);
         if (rc == CRDT_OK) rc = grow(ctx->tile_slot, n * 4, cap);
         if (rc == CRDT_OK) rc = grow(ctx->tile_run, ((n + 1023) / 1024) * 4, cap);

@@ -244,6 +244,15 @@ struct TileGeo {
     bool last, has_next, has_prev, bad;
 };
 
+// A tile's geometry record sits with those of its dispenser shard (tile_take):
+// the shard's tiles, taken in order by the workgroups of one XCD, then share
+// cache lines (four 32-byte records a line) in that XCD's L2, so the geometry
+// load of most taken tiles hits L2 instead of going to memory.
+__device__ __forceinline__ size_t geo_slot(const TileWork& tw, uint32_t g) {
+    const uint32_t S = tw.shards;
+    return (size_t)(g % S) * ((tw.cap + S - 1) / S) + g / S;
+}
+
 // Per-tile geometry, precomputed once per call (tile_geo_kernel) so that a
 // workgroup's dependent chain per tile is dispense -> one 32-byte record ->
 // data loads.
@@ -272,14 +281,16 @@ __global__ __launch_bounds__(256) void tile_geo_kernel(BatchView A, BatchView B,
             r1.z = last | (j1 < ns ? 2u : 0u) | (i0 > 0 ? 4u : 0u);
             r1.w = aoff + boff;
         }
-        tw.geo[2 * (size_t)g] = r0;
-        tw.geo[2 * (size_t)g + 1] = r1;
+        const size_t at = geo_slot(tw, g);
+        tw.geo[2 * at] = r0;
+        tw.geo[2 * at + 1] = r1;
     }
 }
 
 __device__ __forceinline__ TileGeo tile_geo(const BatchView& A, const TileWork& tw, uint32_t g) {
     TileGeo x{};
-    const uint4 r0 = tw.geo[2 * (size_t)g], r1 = tw.geo[2 * (size_t)g + 1];
+    const size_t at = geo_slot(tw, g);
+    const uint4 r0 = tw.geo[2 * at], r1 = tw.geo[2 * at + 1];
     x.d = r0.x;
     x.t = r0.y;
     x.ga = r0.z;
