@@ -107,6 +107,47 @@ __device__ __forceinline__ uint32_t merge_path_in(const uint64_t* dk, const uint
     return lo;
 }
 
+#ifndef CRDT_TILE_GALLOP
+#define CRDT_TILE_GALLOP 1  // 0: every split bisects its whole diagonal (A/B builds)
+#endif
+
+// merge_path_in from a guess g in [lo, hi): probes g, then steps 1, 2, 4 ...
+// away from it until the answer is bracketed, then bisects the bracket.  A
+// tile after its predecessor moves about tile * nd / (nd + ns) along the dst
+// run, so the bracket is a few elements wide and the probes share lines.
+__device__ __forceinline__ uint32_t merge_path_gallop(const uint64_t* dk, const uint64_t* sk, uint32_t k,
+                                                      uint32_t lo, uint32_t hi, uint32_t g) {
+    if (lo >= hi)
+        return lo;
+    g = min(max(g, lo), hi - 1u);
+    if (dk[g] <= sk[k - 1 - g]) {
+        lo = g + 1u;
+        for (uint32_t step = 1;; step <<= 1) {
+            const uint32_t j = g + step;
+            if (j >= hi)
+                break;
+            if (!(dk[j] <= sk[k - 1 - j])) {
+                hi = j;
+                break;
+            }
+            lo = j + 1u;
+        }
+    } else {
+        hi = g;
+        for (uint32_t step = 1;; step <<= 1) {
+            if (step > g - lo)
+                break;
+            const uint32_t j = g - step;
+            if (dk[j] <= sk[k - 1 - j]) {
+                lo = j + 1u;
+                break;
+            }
+            hi = j;
+        }
+    }
+    return merge_path_in(dk, sk, k, lo, hi);
+}
+
 // kSplitRun consecutive tiles per thread: a tile after its document's previous
 // tile searches only the window its predecessor's split bounds (the split
 // moves by at most one tile along each array: i(t) <= i(t+1) <= i(t) + tile),
@@ -149,11 +190,16 @@ __global__ __launch_bounds__(NT) void tile_split_kernel(BatchView A, BatchView B
             const uint32_t nd = live_count(A.offsets, A.counts, d), ns = live_count(B.offsets, B.counts, d);
             const uint32_t k0 = min(t * tw.tile, nd + ns);
             uint32_t lo = k0 > ns ? k0 - ns : 0u, hi = k0 < nd ? k0 : nd;
-            if (d == pd && t == pt + 1u) {  // the previous tile's split bounds this one's
+            const uint64_t* dk = A.keys + A.offsets[d];
+            const uint64_t* sk = B.keys + B.offsets[d];
+            if (CRDT_TILE_GALLOP && d == pd && t == pt + 1u) {  // the previous tile's split bounds this one's
                 lo = max(lo, pi);
                 hi = min(hi, pi + tw.tile);
+                const uint32_t g = pi + (uint32_t)(((uint64_t)tw.tile * nd) / max(nd + ns, 1u));
+                i0 = merge_path_gallop(dk, sk, k0, lo, hi, g);
+            } else {
+                i0 = merge_path_in(dk, sk, k0, lo, hi);
             }
-            i0 = merge_path_in(A.keys + A.offsets[d], B.keys + B.offsets[d], k0, lo, hi);
             j0 = k0 - i0;
         }
         pd = d;

@@ -19,6 +19,7 @@
 #   bintr    boundary_bench with the runtime's interrupt-driven waits (default) and with polling waits
 #   btrace   boundary_bench (C++ mirror ExchangeBatch) with per-phase host stamps, then under a HIP API trace
 #   tsweep   config-4 tile shapes (tools/tile_sweep.py, $TSHAPES as shape:nt_stores)
+#   tab      config-4 exchange timed and kernel-traced per library build ($TLIBS: base or X = tools/libcrdtgpu_X.so)
 #   xab      config-2 exchange store forms A/B (tools/exchange_ab.py)
 #   ptest    pytest -m gpu on $PTEST (a -k expression)
 #   jab      config-2 exchange timed per library build ($JLIBS: base = the product library, X = tools/libcrdtgpu_X.so)
@@ -113,6 +114,17 @@ for r in "$@"; do
       TAILN=12 step tsweep_$TAG 400 python3 tools/tile_sweep.py 16384 ${TSHAPES:-9:1 10:1 9:1 10:1 9:1 10:1} ;;
     tprobe)
       for sh in ${TPROBE:-9}; do TAILN=14 step tprobe_${sh}_$TAG 200 python3 tools/tile_probe.py $sh; done ;;
+    tab)
+      # config-4 exchange per library build ($TLIBS as in jab), HIP-event time and a kernel trace of each
+      for r in 1 2; do for v in ${TLIBS:-base}; do
+        lib=go-crdt-playground_amd/crdtgpu/libcrdtgpu.so; [ "$v" = base ] || lib=tools/libcrdtgpu_$v.so
+        TAILN=3 step tab_${v}_$r 200 env CRDTGPU_LIB=$PWD/$lib python3 tools/tile_sweep.py 16384 9:1
+      done; done
+      for v in ${TLIBS:-base}; do
+        lib=go-crdt-playground_amd/crdtgpu/libcrdtgpu.so; [ "$v" = base ] || lib=tools/libcrdtgpu_$v.so
+        CRDTGPU_LIB=$PWD/$lib TAILN=3 step tabprof_${v}_$TAG 300 rocprofv3 --kernel-trace --stats --output-format csv \
+          -d gpurun_out/tabprof_${v}_$TAG -o run -- python3 tools/tile_sweep.py 16384 9:1
+      done ;;
     xab)
       TAILN=12 step xab_$TAG 400 python3 tools/exchange_ab.py ;;
     ptest)
