@@ -17,6 +17,7 @@
 #   layout   HBM rate vs workgroup -> address mapping (tools/bw_layout)
 #   bthreads boundary_bench at $BTHREADS host threads, with the box's cgroup CPU limits
 #   bintr    boundary_bench with the runtime's interrupt-driven waits (default) and with polling waits
+#   bpf      boundary_bench with and without the host apply's prefetch (CRDT_HOST_NO_PREFETCH; $BPF: name:ENV pairs)
 #   btrace   boundary_bench (C++ mirror ExchangeBatch) with per-phase host stamps, then under a HIP API trace
 #   tsweep   config-4 tile shapes (tools/tile_sweep.py, $TSHAPES as shape:nt_stores)
 #   tab      config-4 exchange timed and kernel-traced per library build ($TLIBS: base or X = tools/libcrdtgpu_X.so)
@@ -105,6 +106,12 @@ for r in "$@"; do
       for v in "default:" "hipcoh:HIP_HOST_COHERENT=1" "coherent:CRDT_HOST_MALLOC_FLAGS=0x40000000" "noncoh:CRDT_HOST_MALLOC_FLAGS=0x80000000" "default2:"; do
         n=${v%%:*}; e=${v#*:}
         TAILN=12 step bcoh_${n}_$TAG 200 env CRDT_TRACE_STAGE=1 $e go-crdt-playground_amd/host/build/boundary_bench 65536
+      done ;;
+    bpf)
+      # host apply with the map elements requested a document ahead (default) vs not
+      for v in ${BPF:-"pf:" "nopf:CRDT_HOST_NO_PREFETCH=1" "pf2:" "nopf2:CRDT_HOST_NO_PREFETCH=1"}; do
+        n=${v%%:*}; e=${v#*:}
+        TAILN=1 step bpf_${n}_$TAG 200 env $e go-crdt-playground_amd/host/build/boundary_bench 65536
       done ;;
     btrace)
       TAILN=30 step bplain_$TAG 200 env CRDT_TRACE_STAGE=1 go-crdt-playground_amd/host/build/boundary_bench 65536
