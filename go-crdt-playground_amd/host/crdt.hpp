@@ -271,6 +271,9 @@ class AWSetDelta : public AWSet {
 // Seconds per phase of the last batch call on this thread (boundary cost).
 struct BoundaryStats {
     double pack_s = 0, device_s = 0, apply_s = 0, call_s = 0;
+    // inside pack_s: the batch's checks (join_batch), the layout (slot offsets),
+    // the per-document packing; inside apply_s: the distinct-states check
+    double batch_s = 0, layout_s = 0, docs_s = 0, distinct_s = 0;
     size_t rank_docs = 0;  // documents interned by rank after a hash collision
 };
 inline BoundaryStats& LastStats() {
@@ -401,6 +404,15 @@ inline Engine::~Engine() {
 }
 
 namespace detail {
+
+// CRDT_HOST_NO_PREFETCH=1: the apply requests nothing ahead (A/B diagnostics).
+inline bool host_prefetch() {
+    static const bool on = [] {
+        const char* e = std::getenv("CRDT_HOST_NO_PREFETCH");
+        return !(e && e[0] == '1');
+    }();
+    return on;
+}
 
 // Fill doc d's slots.  A document's key ids are the order in which its keys
 // first appear over its states (the destination's keys in map order, then
@@ -642,14 +654,7 @@ struct DocPlan {
 // The map elements document d's plan and commit touch -- its destination's
 // and its sources' (their strings name the inserted keys) -- requested ahead:
 // the maps' nodes are scattered over the heap, so the apply is a chain of cache
-// misses unless several are in flight.  (CRDT_HOST_NO_PREFETCH=1: not requested.)
-inline bool host_prefetch() {
-    static const bool on = [] {
-        const char* e = std::getenv("CRDT_HOST_NO_PREFETCH");
-        return !(e && e[0] == '1');
-    }();
-    return on;
-}
+// misses unless several are in flight.
 inline void prefetch_doc(const Batch& b, size_t d) {
     for (uint32_t j = b.dfirst[d], e = b.dfirst[d + 1]; j < e; ++j) __builtin_prefetch(&*b.dit[j], 1);
     for (uint32_t j = b.sfirst[b.src_beg[d]], e = b.sfirst[b.src_beg[d + 1]]; j < e; ++j)
@@ -858,7 +863,9 @@ inline size_t fold_width(int mode, const AWSet& dst, const AWSet* const* srcs, s
 // Returns the destination batch; the sources' arrays are left in the
 // engine's kS_* staging.
 inline crdt_awset_batch pack(Batch& b, Engine& e, bool tombs) {
+    auto t0 = clk::now();
     layout(b, tombs);
+    LastStats().layout_s = secs_since(t0);
     const size_t n = b.n_docs, ns = b.src.size(), R = b.R;
     const size_t nd = b.dfirst[n], nse = b.sfirst[ns], nt = b.tfirst[ns];
     // every input array of the call in one page-locked block: staged by one copy
@@ -888,6 +895,7 @@ inline crdt_awset_batch pack(Batch& b, Engine& e, bool tombs) {
     b.dk = dk, b.da = da, b.dc = dc, b.sk = sk, b.sa = sa, b.sc = sc;
     b.dit = e.iters(0, nd);
     b.sit = e.iters(1, nse);
+    t0 = clk::now();
     parallel_docs(n, [&](size_t lo, size_t hi) {
         DocPacker pk{b, tk, tc, ta, {}, 0, 0, 0, {}, {}, {}};
         for (size_t d = lo; d < hi; ++d) {
@@ -900,6 +908,7 @@ inline crdt_awset_batch pack(Batch& b, Engine& e, bool tombs) {
             }
         }
     });
+    LastStats().docs_s = secs_since(t0);
     size_t ranks = 0;
     for (auto x : b.rank_doc) ranks += x;
     LastStats().rank_docs = ranks;
@@ -998,6 +1007,7 @@ inline void ExchangeBatch(const std::vector<AWSet*>& as, const std::vector<AWSet
     auto t0 = clk::now();
     const auto t_call = t0;
     Batch& b = join_batch(e, as, bs, "ExchangeBatch");
+    LastStats().batch_s = secs_since(t0);
     const crdt_awset_batch ca = pack(b, e, false), cb = src_view(b, e);
     const size_t n = b.n_docs, slots = (size_t)b.dfirst[n] + b.sfirst[n];
     const crdt_awset_out oab = out_arrays(e, kO_OFF, n, b.R, slots);
@@ -1014,6 +1024,7 @@ inline void ExchangeBatch(const std::vector<AWSet*>& as, const std::vector<AWSet
         all.insert(all.end(), bs.begin(), bs.end());
         aliased(all, {}, "ExchangeBatch", e.batch().sorted_states);  // every state distinct
     }
+    LastStats().distinct_s = secs_since(t0);
     apply_docs(
         b, n, false,
         [&](size_t d, DocPlan& p) {  // both plans read the untouched maps ...

@@ -134,9 +134,11 @@ int main(int argc, char** argv) {
     const double merges = 2.0 * n;
     printf("{\"docs\": %zu, \"entries_per_replica\": %d, \"out_entries_per_doc\": %.2f, \"pack_s\": %.6f, "
            "\"device_s\": %.6f, \"apply_s\": %.6f, \"call_s\": %.6f, \"total_s\": %.6f, \"rank_docs\": %zu, \"host_threads\": %u, "
+           "\"host_phases_s\": {\"batch\": %.6f, \"layout\": %.6f, \"pack_docs\": %.6f, \"distinct\": %.6f}, "
            "\"end_to_end_merges_per_s\": %.1f, \"pcie_inclusive_merges_per_s\": %.1f, "
            "\"cpu_same_states_merges_per_s\": %.1f, \"sample_docs_checked\": %zu, \"sample_mismatches\": %zu}\n",
            n, E, (double)live / n, st.pack_s, st.device_s, st.apply_s, st.call_s, total, st.rank_docs, detail::host_threads(),
+           st.batch_s, st.layout_s, st.docs_s, st.distinct_s,
            merges / total, merges / st.device_s, merges / cpu_s, sample.size(), bad);
     return bad ? 1 : 0;
 }
