@@ -111,6 +111,24 @@ def test_tile_equal_key_sets(shaped):
     check_join_and_exchange(shaped, batch_of(R, docs_d), batch_of(R, docs_s), R)
 
 
+def test_tile_disjoint_key_ranges(shaped):
+    """Every dst key below every src key, and the reverse: the merge path runs
+    along one run and then the other, so each tile's split is as far as it gets
+    from the proportional guess the plan's galloping search starts from
+    (tile.hip, merge_path_gallop)."""
+    rng = random.Random(11)
+    R = 2
+    docs_d, docs_s = [], []
+    for nd, ns in ((3 * TILE + 5, 9000), (9000, 3 * TILE + 5), (TILE + 1, 40000), (70, 5 * TILE)):
+        lo = sorted(rng.sample(range(0, 10 ** 6), nd))
+        hi = sorted(rng.sample(range(2 * 10 ** 6, 3 * 10 ** 6), ns))
+        ent = lambda keys: [(k, rng.randrange(R), rng.randint(1, 9)) for k in keys]  # noqa: E731
+        flip = len(docs_d) % 2 == 1
+        docs_d.append((ent(hi if flip else lo), [5, 5]))
+        docs_s.append((ent(lo if flip else hi), [4, 6]))
+    check_join_and_exchange(shaped, batch_of(R, docs_d), batch_of(R, docs_s), R)
+
+
 def test_tile_mixed_with_small_docs_and_slack(shaped, torch):
     """Small (wave path) and large (tile path) documents in one batch, counts <
     slots on both inputs, device-resident through the async ABI."""
