@@ -60,3 +60,16 @@ def test_source_id_follows_the_translation_unit_and_its_headers():
 def test_committed_traffic_table_parses():
     table = json.load(open(os.path.join(ROOT, "profiles", "traffic.json")))
     assert isinstance(table, list) and all("kernel" in e and "docs" in e for e in table)
+
+
+def test_committed_table_covers_every_timed_kernel_at_this_tree():
+    """Every bench leg's dominant kernel, at the source id of this tree, has its
+    PMC entry in profiles/traffic.json -- so the line's roofline.traffic comes
+    from a profile of exactly these sources (a kernel edit needs
+    `tools/gpu_run.sh pmcall` before this passes again)."""
+    path = os.path.join(ROOT, "profiles", "traffic.json")
+    for c, cls in ((2, bench.Config2), (3, bench.Config3), (4, bench.Config4), (5, bench.Config5)):
+        W = object.__new__(cls)  # class defaults: the forms the bench times
+        b, note, e = bench._traffic(path, c, bench.DEFAULT_DOCS[c], W)
+        assert b is not None, "config %d: %s" % (c, note)
+        assert os.path.exists(os.path.join(ROOT, e["profile"])), e["profile"]
