@@ -125,12 +125,12 @@ for r in "$@"; do
       # config-4 exchange per library build ($TLIBS as in jab), HIP-event time and a kernel trace of each
       for r in 1 2; do for v in ${TLIBS:-base}; do
         lib=go-crdt-playground_amd/crdtgpu/libcrdtgpu.so; [ "$v" = base ] || lib=tools/libcrdtgpu_$v.so
-        TAILN=3 step tab_${v}_$r 200 env CRDTGPU_LIB=$PWD/$lib python3 tools/tile_sweep.py 16384 9:1
+        TAILN=3 step tab_${v}_$r 200 env CRDTGPU_LIB=$PWD/$lib python3 tools/tile_sweep.py 16384 ${TSHAPE:-9:1}
       done; done
       for v in ${TLIBS:-base}; do
         lib=go-crdt-playground_amd/crdtgpu/libcrdtgpu.so; [ "$v" = base ] || lib=tools/libcrdtgpu_$v.so
         CRDTGPU_LIB=$PWD/$lib TAILN=3 step tabprof_${v}_$TAG 300 rocprofv3 --kernel-trace --stats --output-format csv \
-          -d gpurun_out/tabprof_${v}_$TAG -o run -- python3 tools/tile_sweep.py 16384 9:1
+          -d gpurun_out/tabprof_${v}_$TAG -o run -- python3 tools/tile_sweep.py 16384 ${TSHAPE:-9:1}
       done ;;
     xab)
       TAILN=12 step xab_$TAG 400 python3 tools/exchange_ab.py ;;
