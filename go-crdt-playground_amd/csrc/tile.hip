@@ -110,6 +110,9 @@ __device__ __forceinline__ uint32_t merge_path_in(const uint64_t* dk, const uint
 #ifndef CRDT_TILE_GALLOP
 #define CRDT_TILE_GALLOP 1  // 0: every split bisects its whole diagonal (A/B builds)
 #endif
+#ifndef CRDT_TILE_GALLOP_HEAD
+#define CRDT_TILE_GALLOP_HEAD CRDT_TILE_GALLOP  // 0: a run's first split bisects (A/B builds)
+#endif
 
 // merge_path_in from a guess g in [lo, hi): probes g, then steps 1, 2, 4 ...
 // away from it until the answer is bracketed, then bisects the bracket.  A
@@ -197,6 +200,8 @@ __global__ __launch_bounds__(NT) void tile_split_kernel(BatchView A, BatchView B
                 hi = min(hi, pi + tw.tile);
                 const uint32_t g = pi + (uint32_t)(((uint64_t)tw.tile * nd) / max(nd + ns, 1u));
                 i0 = merge_path_gallop(dk, sk, k0, lo, hi, g);
+            } else if (CRDT_TILE_GALLOP_HEAD) {  // a run's first tile: from the proportional point of its diagonal
+                i0 = merge_path_gallop(dk, sk, k0, lo, hi, (uint32_t)(((uint64_t)k0 * nd) / max(nd + ns, 1u)));
             } else {
                 i0 = merge_path_in(dk, sk, k0, lo, hi);
             }

@@ -65,6 +65,8 @@ def test_gallop_matches_bisection(seed):
             k = min(t * tile, nd + ns)
             lo, hi = max(0, k - ns), min(k, nd)
             full = merge_path_in(dk, sk, k, lo, hi)
+            # a run's first tile: from the proportional point of the whole diagonal
+            assert merge_path_gallop(dk, sk, k, lo, hi, (k * nd) // max(nd + ns, 1)) == full
             if prev is not None:  # the kernel's windowed call for tile t after tile t-1
                 g = prev + (tile * nd) // max(nd + ns, 1)
                 got = merge_path_gallop(dk, sk, k, max(lo, prev), min(hi, prev + tile), g)
