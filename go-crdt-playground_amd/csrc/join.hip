@@ -29,6 +29,9 @@ namespace crdt {
 // 128-byte lines, 0 = off).  The folds gain nothing from it (their stores are
 // not what binds them: profiles/r05b_fold_stage_pad_ab.log), so they keep
 // their own store forms.
+#ifndef CRDT_JOIN_WAVE_PUSH
+#define CRDT_JOIN_WAVE_PUSH 1  // 0: one worklist atomic per large document (A/B builds)
+#endif
 #ifndef CRDT_JOIN_PAD_STORES
 #define CRDT_JOIN_PAD_STORES 1
 #endif
@@ -306,6 +309,7 @@ __global__ __launch_bounds__(WAVES * 64) CRDT_JOIN_WPE_ATTR void join_wave_kerne
     const MetaVec mv = meta_vec_issue(dst, src, first, WAVES, lane);
 
     auto push_large = [&](uint32_t dd) {
+        if (CRDT_JOIN_WAVE_PUSH) return;  // pushed below, all at once
         if (lane == 0) {
             if (no_large)
                 atomicOr(wk.status, kErrHint);
@@ -313,6 +317,32 @@ __global__ __launch_bounds__(WAVES * 64) CRDT_JOIN_WPE_ATTR void join_wave_kerne
                 push_work(wk, dd, n_docs);
         }
     };
+    if (CRDT_JOIN_WAVE_PUSH) {
+        // The wave's large documents (lane i: document first + i * WAVES) go to
+        // the worklist with ONE atomic on its counter: config 4 pushes 10,800
+        // documents, and one counter word takes ~88 M atomics/s, so a push per
+        // document serialised ~0.1 ms of the launch on that word.
+        const uint32_t dn_l = dst.counts ? mv.dend : mv.dend - mv.doff;
+        const uint32_t sn_l = src.counts ? mv.send : mv.send - mv.soff;
+        const bool large = lane < cnt && (dn_l > 64 || sn_l > 64);
+        const uint64_t bl = ballot(large);
+        if (bl) {
+            if (no_large) {
+                if (lane == 0) atomicOr(wk.status, kErrHint);
+            } else {
+                uint32_t base = 0;
+                if (lane == 0) base = atomicAdd(wk.wl_count, (uint32_t)__builtin_popcountll(bl));
+                base = (uint32_t)__builtin_amdgcn_readfirstlane((int)base);
+                const uint32_t slot = base + (uint32_t)__builtin_popcountll(bl & lt);
+                if (large) {  // bounded as push_work
+                    if (slot < n_docs)
+                        wk.worklist[slot] = first + lane * WAVES;
+                    else
+                        atomicOr(wk.status, kErrWorkspace);
+                }
+            }
+        }
+    }
 
     JoinMeta m = meta_of(dst, src, mv, 0);
     uint32_t d = first;
