@@ -117,21 +117,44 @@ class AWSetBatch:
         return int(o[-1]) - int(o[0])
 
 
+def pinned_zeros(n, dtype):
+    """A zeroed numpy array in page-locked host memory (crdt_host_alloc), freed
+    with the array.  The *_batch calls stage inputs that lie in one such block
+    with one copy, and write packed outputs that lie in such blocks from the
+    gather kernel (api.cpp, fetch_outputs)."""
+    import weakref
+
+    from . import abi
+
+    lib = abi.lib()
+    nbytes = max(int(n), 1) * np.dtype(dtype).itemsize
+    p = ctypes.c_void_p()
+    rc = lib.crdt_host_alloc(nbytes, ctypes.byref(p))
+    if rc != 0:
+        raise MemoryError("crdt_host_alloc(%d): %d" % (nbytes, rc))
+    buf = (ctypes.c_char * nbytes).from_address(p.value)
+    arr = np.frombuffer(buf, dtype=dtype, count=max(int(n), 1))
+    arr[:] = 0
+    weakref.finalize(buf, lib.crdt_host_free, ctypes.c_void_p(p.value))
+    return arr
+
+
 class OutBuffers:
     """Output of a join/fold: n_docs docs, `slots` capacity, numpy or torch.
     shared_keys: another OutBuffers whose key column this one uses (the two
     outputs of an exchange hold the same keys at the same slots,
-    crdt_awset_exchange_async)."""
+    crdt_awset_exchange_async).  pinned: host arrays in page-locked memory."""
 
-    def __init__(self, n_docs, R, slots, device=None, shared_keys=None):
+    def __init__(self, n_docs, R, slots, device=None, shared_keys=None, pinned=False):
         self.R, self.n_docs, self.slots = int(R), int(n_docs), int(slots)
         if device is None:
-            self.offsets = np.zeros(n_docs + 1, dtype=U32)
-            self.counts = np.zeros(n_docs, dtype=U32)
-            self.keys = np.zeros(max(slots, 1), dtype=U64)
-            self.actors = np.zeros(max(slots, 1), dtype=U32)
-            self.counters = np.zeros(max(slots, 1), dtype=U64)
-            self.vv = np.zeros(max(n_docs * R, 1), dtype=U64)
+            z = pinned_zeros if pinned else (lambda n, dt: np.zeros(n, dtype=dt))
+            self.offsets = z(n_docs + 1, U32)
+            self.counts = z(n_docs, U32)[:n_docs]
+            self.keys = z(max(slots, 1), U64)
+            self.actors = z(max(slots, 1), U32)
+            self.counters = z(max(slots, 1), U64)
+            self.vv = z(max(n_docs * R, 1), U64)
         else:
             import torch
 

@@ -167,20 +167,22 @@ class Engine:
                                             ctypes.byref(cb), _stream(stream)), "crdt_gen_zipf_async")
 
     # -- host buffers, synchronous ----------------------------------------
-    def join(self, dst: AWSetBatch, src: AWSetBatch) -> OutBuffers:
+    def join(self, dst: AWSetBatch, src: AWSetBatch, pinned: bool = False) -> OutBuffers:
+        """Host buffers; pinned: the output in page-locked memory (crdt_host_alloc)."""
         dst, src = dst.numpy(), src.numpy()
-        out = OutBuffers(dst.n_docs, dst.R, int(dst.offsets[-1]) + int(src.offsets[-1]))
+        out = OutBuffers(dst.n_docs, dst.R, int(dst.offsets[-1]) + int(src.offsets[-1]), pinned=pinned)
         d, s, o = dst.c(), src.c(), out.c()
         check(self._lib.crdt_awset_join_batch(self._ctx, ctypes.byref(d), ctypes.byref(s), ctypes.byref(o)),
               "crdt_awset_join_batch")
         return out
 
-    def exchange(self, a: AWSetBatch, b: AWSetBatch, shared_keys: bool = False):
-        """Host buffers: (a <- b, b <- a); shared_keys: both outputs use one key column."""
+    def exchange(self, a: AWSetBatch, b: AWSetBatch, shared_keys: bool = False, pinned: bool = False):
+        """Host buffers: (a <- b, b <- a); shared_keys: both outputs use one key column;
+        pinned: the outputs in page-locked memory (crdt_host_alloc)."""
         a, b = a.numpy(), b.numpy()
         slots = int(a.offsets[-1]) + int(b.offsets[-1])
-        o1 = OutBuffers(a.n_docs, a.R, slots)
-        o2 = OutBuffers(a.n_docs, a.R, slots, shared_keys=o1 if shared_keys else None)
+        o1 = OutBuffers(a.n_docs, a.R, slots, pinned=pinned)
+        o2 = OutBuffers(a.n_docs, a.R, slots, shared_keys=o1 if shared_keys else None, pinned=pinned)
         ca, cb, c1, c2 = a.c(), b.c(), o1.c(), o2.c()
         check(self._lib.crdt_awset_exchange_batch(self._ctx, ctypes.byref(ca), ctypes.byref(cb), ctypes.byref(c1),
                                                   ctypes.byref(c2)), "crdt_awset_exchange_batch")
@@ -202,9 +204,9 @@ class Engine:
                                                ctypes.byref(cto) if cto else None), "crdt_awset_apply_batch")
         return out, tout
 
-    def fold(self, mode: int, dst: AWSetBatch, srcs: SrcBatch) -> OutBuffers:
+    def fold(self, mode: int, dst: AWSetBatch, srcs: SrcBatch, pinned: bool = False) -> OutBuffers:
         dst, srcs = dst.numpy(), srcs.numpy()
-        out = OutBuffers(dst.n_docs, dst.R, srcs.out_slots(dst))
+        out = OutBuffers(dst.n_docs, dst.R, srcs.out_slots(dst), pinned=pinned)
         d, s, o = dst.c(), srcs.c(), out.c()
         check(self._lib.crdt_awset_fold_batch(self._ctx, int(mode), ctypes.byref(d), ctypes.byref(s),
                                               ctypes.byref(o)), "crdt_awset_fold_batch")

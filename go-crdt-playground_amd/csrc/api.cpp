@@ -27,8 +27,10 @@ uint32_t tile_positions(uint32_t shape);
 hipError_t sort_storage(uint32_t n_docs, uint32_t n_slots, size_t* bytes);
 hipError_t launch_check_order(const uint32_t* off, const uint32_t* cnt, uint32_t n, const uint64_t* keys,
                               uint32_t* status, uint32_t n_cu, hipStream_t stream);
-hipError_t launch_pack_out(const OutView& in, const uint32_t* poff, uint32_t n, const OutView& out, uint32_t n_cu,
-                           hipStream_t stream);
+hipError_t launch_pack_scan(const uint32_t* off, const uint32_t* cnt, uint32_t n, uint32_t* poff, uint32_t* host_off,
+                            const uint32_t* gate, hipStream_t stream);
+hipError_t launch_pack_out(const OutView& in, const uint32_t* poff, uint32_t n, uint32_t R, const OutView& out,
+                           const uint32_t* gate, uint32_t n_cu, hipStream_t stream);
 hipError_t launch_sort(const BatchView& in, uint32_t n_slots, const OutView& out, void* temp, size_t temp_bytes,
                        uint32_t* ends, uint32_t* idx, uint32_t* status, uint32_t n_cu, hipStream_t stream);
 hipError_t launch_apply(const BatchView& st, const TombView& tb, const ApplyOps& ops, const OutView& out,
@@ -109,19 +111,38 @@ struct DevBuf {
 // they cover (Stager), because each runtime H2D copy call costs the host 1-7
 // ms before its DMA is even submitted, whatever its size
 // (profiles/r05i_boundary_timeline.txt), while the span moves at PCIe rate.
+// Each block also keeps its device-side address: a host-path call whose outputs
+// lie in such blocks has its packed results written there by the gather kernel
+// (pack.hip) instead of copied back by runtime copy calls.
+struct HostBlock {
+    size_t size;
+    uintptr_t dev;  // hipHostGetDevicePointer of the base (0: none)
+};
 std::mutex g_host_mu;
-std::map<uintptr_t, size_t> g_host_blocks;
+std::map<uintptr_t, HostBlock> g_host_blocks;
 
-bool host_block(const void* p, uintptr_t& base, size_t& size) {
+bool host_block(const void* p, uintptr_t& base, size_t& size, uintptr_t* dev = nullptr) {
     const uintptr_t a = (uintptr_t)p;
     std::lock_guard<std::mutex> lk(g_host_mu);
     auto it = g_host_blocks.upper_bound(a);
     if (it == g_host_blocks.begin()) return false;
     --it;
-    if (a >= it->first + it->second) return false;
+    if (a >= it->first + it->second.size) return false;
     base = it->first;
-    size = it->second;
+    size = it->second.size;
+    if (dev) *dev = it->second.dev;
     return true;
+}
+
+// The device address of host range [p, p + bytes) when all of it lies in one
+// crdt_host_alloc block (0 otherwise).
+uintptr_t host_dev_addr(const void* p, size_t bytes) {
+    uintptr_t base = 0, dev = 0;
+    size_t size = 0;
+    if (!p || !host_block(p, base, size, &dev) || !dev) return 0;
+    const uintptr_t a = (uintptr_t)p;
+    if (a + bytes > base + size) return 0;
+    return dev + (a - base);
 }
 
 
@@ -149,6 +170,10 @@ struct crdt_ctx {
     bool tile_nt_stores = true;               // crdt_ctx_set_option("join_tile_nt_stores")
     uint32_t tile_split_bpc = 4;              // crdt_ctx_set_option("join_tile_split_blocks_per_cu")
     uint32_t tile_shards = 8;                 // crdt_ctx_set_option("join_tile_dispensers")
+    uint32_t tile_max_passes = 256;           // crdt_ctx_set_option("join_tile_max_passes")
+    // the tiles of the join this host-path call is about to launch, counted from
+    // its host arrays (0: unknown, an _async call: bounded instead, join_common)
+    uint64_t call_tiles = 0;
     size_t scratch_slots = 0;
     uint32_t max_doc_entries = 0xFFFFFFFFu;  // caller's promise (crdt_ctx_set_max_doc_entries)
     uint32_t join_docs_per_wave = 8;          // crdt_ctx_set_option("join_docs_per_wave")
@@ -159,8 +184,14 @@ struct crdt_ctx {
     uint32_t probe_blocks_per_cu = 16;        // crdt_ctx_set_option("probe_blocks_per_cu")
     bool probe_slab = false;                  // crdt_ctx_set_option("probe_slab")
     bool pack_outputs = false;                // crdt_ctx_set_option("pack_batch_outputs")
-    // staging for the *_batch host path
-    DevBuf stage[32];
+    bool span_staging = true;                 // crdt_ctx_set_option("span_staging")
+    // staging for the *_batch host path: per-array buffers, and the device image
+    // of the part of one crdt_host_alloc block a call's inputs cover (Stager)
+    DevBuf stage[48];
+    DevBuf span_img;
+    // set by a *_batch call around its merge launch: the merge's first kernel is
+    // gated on the status word its order checks wrote (Work::gate)
+    bool call_gate = false;
     hipStream_t stream = nullptr;
     // Ordering of the shared workspace across streams: the last call's stream
     // and an event recorded after its launches.  A call on another stream
@@ -202,6 +233,7 @@ Work make_work(crdt_ctx* ctx) {
     w.worklist = ctx->worklist.as<uint32_t>();
     w.defer_count = ctx->ws.as<uint32_t>(8);
     w.defer = ctx->defer.as<uint32_t>();
+    w.gate = ctx->call_gate ? w.status : nullptr;
     return w;
 }
 
@@ -308,6 +340,7 @@ int crdt_ctx_create(int device, crdt_ctx** out) {
                       &ctx->tile_slot, &ctx->tile_run, &ctx->sort_tmp, &ctx->sort_idx, &ctx->sort_ends})
         b->retired = &ctx->retired;
     for (auto& b : ctx->stage) b.retired = &ctx->retired;
+    ctx->span_img.retired = &ctx->retired;
     int rc = set_device(ctx);
     hipDeviceProp_t prop;
     if (rc == CRDT_OK && hipGetDeviceProperties(&prop, device) == hipSuccess) ctx->n_cu = prop.multiProcessorCount;
@@ -346,6 +379,7 @@ void crdt_ctx_destroy(crdt_ctx* ctx) {
                       &ctx->sort_tmp, &ctx->sort_idx, &ctx->sort_ends})
         b->release();
     for (auto& b : ctx->stage) b.release();
+    ctx->span_img.release();
     delete ctx;
 }
 
@@ -370,9 +404,14 @@ int crdt_ctx_set_option(crdt_ctx* ctx, const char* name, int64_t value) {
         ctx->join_docs_per_wave = (uint32_t)value;
         return CRDT_OK;
     }
-    if (!strcmp(name, "join_tile_capacity")) {  // tiles of 2048 merged positions; more -> block kernel
+    if (!strcmp(name, "join_tile_capacity")) {  // tiles per pass of the tile path (workspace: 56 B a tile)
         if (value < 1 || value > (1ll << 28)) return CRDT_E_INVALID;
         ctx->tile_cap = (uint32_t)value;
+        return CRDT_OK;
+    }
+    if (!strcmp(name, "join_tile_max_passes")) {  // more tiles than passes x capacity -> block kernel
+        if (value < 1 || value > 65536) return CRDT_E_INVALID;
+        ctx->tile_max_passes = (uint32_t)value;
         return CRDT_OK;
     }
     if (!strcmp(name, "join_tile_shape")) {  // threads x positions: look-back per tile 0: 512x4, 1: 256x4, 2: 256x8,
@@ -402,6 +441,10 @@ int crdt_ctx_set_option(crdt_ctx* ctx, const char* name, int64_t value) {
     }
     if (!strcmp(name, "pack_batch_outputs")) {  // *_batch joins / exchanges / folds: live entries only, packed
         ctx->pack_outputs = value != 0;
+        return CRDT_OK;
+    }
+    if (!strcmp(name, "span_staging")) {  // *_batch inputs in one crdt_host_alloc block: one copy of their span
+        ctx->span_staging = value != 0;
         return CRDT_OK;
     }
     if (!strcmp(name, "probe_slab")) {  // bandwidth probes: one contiguous slab per workgroup
@@ -473,17 +516,33 @@ static int join_common(crdt_ctx* ctx, const crdt_awset_batch* dst, const crdt_aw
     const bool tiles = !no_large && ctx->join_tiles;
     if (tiles) {
         const size_t n = std::max<size_t>(dst->n_docs, 1);
-        rc = grow(ctx->tile_desc, (size_t)ctx->tile_cap * 16, cap);
+        rc = grow(ctx->tile_desc, ((size_t)ctx->tile_cap + 1) * 16, cap);  // (+1: the next pass's first split)
         if (rc == CRDT_OK) rc = grow(ctx->tile_geo, ((size_t)ctx->tile_cap + 8) * 32, cap);  // (+8: geo_slot)
         if (rc == CRDT_OK) rc = grow(ctx->tile_flags, (size_t)ctx->tile_cap * 8, cap);
         if (rc == CRDT_OK) rc = grow(ctx->tile_slot, n * 4, cap);
         if (rc == CRDT_OK) rc = grow(ctx->tile_run, ((n + 1023) / 1024) * 4, cap);
         if (rc != CRDT_OK) return rc;
         uint32_t* w = ctx->ws.as<uint32_t>(0);
+        // Passes of tile_cap tiles: as many as the call's tiles can need.  A host-path
+        // call counted them (ctx->call_tiles); otherwise a document of nd + ns merged
+        // positions has ceil((nd + ns) / T) tiles, and a batch's slots are < 2^32 per
+        // side, so a call has at most 2^33 / T + n_docs -- or, under the caller's
+        // max_doc_entries promise, n_docs * ceil(2 max / T).  Passes past the call's
+        // tiles return at once.  The block kernel is launched behind them (gated on
+        // the plan's fallback word) unless the passes hold every tile a call can have
+        // without trusting the promise: beyond them (tile_max_passes, or a broken
+        // promise) it takes the worklist.
+        const uint64_t T = tile_positions(ctx->tile_shape);
+        const uint64_t hard = ctx->call_tiles ? ctx->call_tiles : (1ull << 33) / T + dst->n_docs;
+        uint64_t bound = hard;
+        if (!ctx->call_tiles && ctx->max_doc_entries != 0xFFFFFFFFu)
+            bound = std::min<uint64_t>(bound, (uint64_t)dst->n_docs * ((2ull * ctx->max_doc_entries + T - 1) / T));
+        auto passes_for = [&](uint64_t t) { return std::max<uint64_t>(1, (t + ctx->tile_cap - 1) / ctx->tile_cap); };
+        const uint32_t passes = (uint32_t)std::min<uint64_t>(passes_for(bound), ctx->tile_max_passes);
         tw = TileWork{ctx->tile_desc.as<uint4>(), ctx->tile_geo.as<uint4>(), ctx->tile_flags.as<uint64_t>(), ctx->tile_slot.as<uint32_t>(),
-                      ctx->tile_run.as<uint32_t>(), w + 3, w + 8, w + 5, ctx->tile_cap,
+                      ctx->tile_run.as<uint32_t>(), w + 3, w + 8, w + 5, w + 6, ctx->tile_cap,
                       tile_positions(ctx->tile_shape), ctx->tile_shape, ctx->tile_nt_stores ? 1u : 0u,
-                      ctx->tile_split_bpc, ctx->tile_shards};
+                      ctx->tile_split_bpc, ctx->tile_shards, 0u, passes, passes_for(hard) <= passes ? 1u : 0u};
     }
     // the per-call counters are read only by the large-document paths
     if (!no_large && launch_reset_work(ctx->ws.as<uint32_t>(0), s) != hipSuccess) return CRDT_E_HIP;
@@ -747,8 +806,10 @@ int crdt_host_alloc(size_t bytes, void** out) {
         return e ? (unsigned)std::strtoul(e, nullptr, 0) : (unsigned)hipHostMallocDefault;
     }();
     if (hipHostMalloc(out, bytes, flags) != hipSuccess) return CRDT_E_NOMEM;
+    void* dev = nullptr;
+    if (hipHostGetDevicePointer(&dev, *out, 0) != hipSuccess) dev = nullptr;
     std::lock_guard<std::mutex> lk(g_host_mu);
-    g_host_blocks[(uintptr_t)*out] = bytes;
+    g_host_blocks[(uintptr_t)*out] = HostBlock{bytes, (uintptr_t)dev};
     return CRDT_OK;
 }
 
@@ -790,7 +851,7 @@ int crdt_clock_probe(crdt_ctx* ctx, double* mhz) {
 // Pointers, slot bounds, live counts and (keys = true) the key order.  The
 // *_batch calls check only the layout here (O(documents)) and the key order
 // on the device after the upload (pack.hip, check_order_kernel), whose verdict
-// they read back before launching a merge (order_gate).
+// the merge's first kernel reads before doing anything (Work::gate).
 static int validate_batch(const crdt_awset_batch* b, bool keys) {
     if (!b || !b->offsets || b->R == 0 || b->R > CRDT_MAX_R) return CRDT_E_INVALID;
     if (b->n_docs && (!b->vv || ((b->offsets[b->n_docs] > b->offsets[0]) && (!b->keys || !b->actors || !b->counters))))
@@ -871,50 +932,58 @@ struct PhaseClock {
     }
 };
 
-constexpr int kSpanSlot = 31;  // ctx->stage[kSpanSlot]: the device image of a host block's span
+constexpr int kStageSlots = 48;  // ctx->stage: per-array device buffers of one call
 
+// The device copies of a host-path call's arrays.  Input arrays that lie in one
+// crdt_host_alloc block are staged by ONE copy of the span they cover: each
+// runtime H2D copy call costs the host 1-7 ms before its DMA is even
+// submitted, whatever its size (profiles/r05i_boundary_timeline.txt), while
+// the span moves at PCIe rate.  Other arrays, and output rooms, get a buffer of
+// their own.  A call runs its input staging twice: first planning (plan():
+// nothing is allocated, only the span the call's arrays cover is measured),
+// then for real, so the device image is the size of that span, not of the
+// whole block.
 struct Stager {
     crdt_ctx* ctx;
+    bool planning = false;
     int next = 0;
     int rc = CRDT_OK;
-    // the host block of this call's first staged array (span staging), the
-    // device image of that whole block, and the part of it to copy
-    uintptr_t blk = 0;
+    uintptr_t blk = 0;  // the host block of the call's inputs (the first one met)
     size_t blk_size = 0;
+    size_t lo = SIZE_MAX, hi = 0;  // the span of it the call covers
+    size_t img_lo = 0;             // block offset of the device image's first byte
     char* dimg = nullptr;
-    size_t lo = SIZE_MAX, hi = 0;
     bool flushed = false;
     template <typename T>
     T* put(const T* host, size_t n) {  // allocate + copy in (n elements)
         if (rc != CRDT_OK) return nullptr;
         static const bool trace = std::getenv("CRDT_TRACE_STAGE") != nullptr;  // diagnostics: host time per step
         static const bool span = std::getenv("CRDT_NO_SPAN_STAGING") == nullptr;
-        if (span && host && n) {
-            if (!blk) {
+        const uintptr_t a = (uintptr_t)host;
+        const size_t bytes = n * sizeof(T);
+        if (planning) {
+            if (span && ctx->span_staging && host && n) {
                 uintptr_t b0 = 0;
                 size_t sz = 0;
-                if (host_block(host, b0, sz) && sz <= ((size_t)4 << 30)) {  // (a larger block: array by array)
-                    rc = ctx->stage[kSpanSlot].reserve(sz);
-                    if (rc != CRDT_OK) return nullptr;
+                if (!blk && host_block(host, b0, sz)) {
                     blk = b0;
                     blk_size = sz;
-                    dimg = ctx->stage[kSpanSlot].as<char>();
+                }
+                if (blk && a >= blk && a + bytes <= blk + blk_size) {
+                    lo = std::min(lo, (size_t)(a - blk));
+                    hi = std::max(hi, (size_t)(a - blk) + bytes);
                 }
             }
-            const uintptr_t a = (uintptr_t)host, bytes = n * sizeof(T);
-            if (blk && a >= blk && a + bytes <= blk + blk_size) {
-                const size_t off = a - blk;
-                if (flushed) {  // staged after the span went: its own copy, into the same image
-                    if (hipMemcpyAsync(dimg + off, host, bytes, hipMemcpyHostToDevice, ctx->stream) != hipSuccess)
-                        rc = CRDT_E_HIP;
-                } else {
-                    lo = std::min(lo, off);
-                    hi = std::max(hi, off + (size_t)bytes);
-                }
-                return reinterpret_cast<T*>(dimg + off);
-            }
+            return nullptr;
         }
-        if (next >= kSpanSlot) {
+        if (dimg && host && n && a >= blk + img_lo && a + bytes <= blk + hi) {
+            const size_t off = a - blk - img_lo;
+            // staged after the span went: its own copy, into the same image
+            if (flushed && hipMemcpyAsync(dimg + off, host, bytes, hipMemcpyHostToDevice, ctx->stream) != hipSuccess)
+                rc = CRDT_E_HIP;
+            return reinterpret_cast<T*>(dimg + off);
+        }
+        if (next >= kStageSlots) {
             rc = CRDT_E_INVALID;
             return nullptr;
         }
@@ -923,11 +992,11 @@ struct Stager {
         rc = b.reserve(std::max<size_t>(n, 1) * sizeof(T));
         if (rc != CRDT_OK) return nullptr;
         const auto t1 = std::chrono::steady_clock::now();
-        if (host && n && hipMemcpyAsync(b.p, host, n * sizeof(T), hipMemcpyHostToDevice, ctx->stream) != hipSuccess)
+        if (host && n && hipMemcpyAsync(b.p, host, bytes, hipMemcpyHostToDevice, ctx->stream) != hipSuccess)
             rc = CRDT_E_HIP;
         if (trace) {
             const auto t2 = std::chrono::steady_clock::now();
-            fprintf(stderr, "stage[%d] %zu B: reserve %.3f ms, copy call %.3f ms\n", next - 1, n * sizeof(T),
+            fprintf(stderr, "stage[%d] %zu B: reserve %.3f ms, copy call %.3f ms\n", next - 1, bytes,
                     std::chrono::duration<double, std::milli>(t1 - t0).count(),
                     std::chrono::duration<double, std::milli>(t2 - t1).count());
         }
@@ -937,14 +1006,25 @@ struct Stager {
     T* room(size_t n) {
         return put<T>(nullptr, n);
     }
+    // Run the call's input staging `f` planning, size the span's image, then run it for real.
+    template <typename F>
+    void plan(F&& f) {
+        planning = true;
+        f();
+        planning = false;
+        if (rc == CRDT_OK && blk && hi > lo) {
+            img_lo = lo & ~(size_t)255;  // (the image keeps the block's 256-byte alignment)
+            if (hi - img_lo <= ((size_t)4 << 30)) {  // (a larger span: array by array)
+                rc = ctx->span_img.reserve(hi - img_lo);
+                if (rc == CRDT_OK) dimg = ctx->span_img.as<char>();
+            }
+        }
+        f();
+    }
     // Copy the span of the host block that this call's arrays cover (one call).
     void flush() {
-        if (rc != CRDT_OK || flushed || !blk || hi <= lo) {
-            flushed = blk != 0;
-            return;
-        }
-        const size_t a = lo & ~(size_t)255;  // (the image keeps the block's alignment)
-        if (hipMemcpyAsync(dimg + a, reinterpret_cast<const char*>(blk) + a, hi - a, hipMemcpyHostToDevice,
+        if (rc == CRDT_OK && !flushed && dimg &&
+            hipMemcpyAsync(dimg, reinterpret_cast<const char*>(blk) + img_lo, hi - img_lo, hipMemcpyHostToDevice,
                            ctx->stream) != hipSuccess)
             rc = CRDT_E_HIP;
         flushed = true;
@@ -993,47 +1073,98 @@ int fetch_out(const crdt_awset_out* h, const crdt_awset_out& d, uint32_t n_docs,
 }
 
 // The key order of a staged batch (ranges off[r] .. + counts or off[r + 1]),
-// checked on the device; a violation reads back as CRDT_E_UNSORTED.
+// checked on the device; a violation sets kErrUnsorted in the status word, which
+// closes the merge's gate (Work::gate) and reads back as CRDT_E_UNSORTED.
 int check_order(crdt_ctx* ctx, const uint32_t* off, const uint32_t* cnt, uint32_t n, const uint64_t* keys) {
     return hip_err(launch_check_order(off, cnt, n, keys, ctx->ws.as<uint32_t>(64), (uint32_t)ctx->n_cu, ctx->stream));
 }
 
-// The order checks' verdict, read back before any merge kernel is launched:
-// the merge kernels assume strictly ascending keys, so a batch that is not
-// never reaches them (one small sync; the uploads precede the merge anyway).
-int order_gate(crdt_ctx* ctx, int rc) {
-    return rc == CRDT_OK ? crdt_ctx_sync(ctx, ctx->stream) : rc;
+// The merge launch of a host-path call, gated on the device by its order checks.
+template <typename F>
+int gated(crdt_ctx* ctx, F&& launch) {
+    ctx->call_gate = true;
+    const int rc = launch();
+    ctx->call_gate = false;
+    ctx->call_tiles = 0;
+    return rc;
 }
 
-// Download a merge output: at its capacity offsets, or (pack_batch_outputs)
-// only the live entries, gathered on the device at offsets = the prefix sums
-// of the counts, so PCIe moves live entries only.
-int fetch_merge_out(crdt_ctx* ctx, Stager& st, const crdt_awset_out* h, const crdt_awset_out& d, uint32_t n,
-                    uint32_t R, size_t slots, bool keys = true) {
-    if (!ctx->pack_outputs) return fetch_out(h, d, n, R, slots, ctx->stream, keys);
-    int rc = get(h->counts, d.counts, n, ctx->stream);
-    if (rc == CRDT_OK && hipStreamSynchronize(ctx->stream) != hipSuccess) rc = CRDT_E_HIP;
-    if (rc != CRDT_OK) return rc;
-    uint64_t tot = 0;
-    h->offsets[0] = 0;
-    for (uint32_t i = 0; i < n; ++i) {
-        tot += h->counts[i];
-        if (tot > slots) {  // only after a failed merge (e.g. unsorted input): report that failure
-            const int sync = crdt_ctx_sync(ctx, ctx->stream);
-            return sync != CRDT_OK ? sync : CRDT_E_CAPACITY;
-        }
-        h->offsets[i + 1] = (uint32_t)tot;
+// Tiles the join of host batches a <- b launches (tile.hip: ceil((nd + ns) / T)
+// per document with more than 64 live entries on a side), so the tile path
+// launches exactly the passes it needs (join_common).
+uint64_t host_tiles(const crdt_ctx* ctx, const crdt_awset_batch* a, const crdt_awset_batch* b) {
+    if (ctx->max_doc_entries <= 64 || !ctx->join_tiles) return 0;
+    const uint64_t T = tile_positions(ctx->tile_shape);
+    uint64_t t = 0;
+    for (uint32_t d = 0; d < a->n_docs; ++d) {
+        const uint64_t nd = a->counts ? a->counts[d] : a->offsets[d + 1] - a->offsets[d];
+        const uint64_t ns = b->counts ? b->counts[d] : b->offsets[d + 1] - b->offsets[d];
+        if (nd > 64 || ns > 64) t += (nd + ns + T - 1) / T;
     }
-    const uint32_t* poff = st.put(h->offsets, (size_t)n + 1);
-    const crdt_awset_out p{nullptr, nullptr, st.room<uint64_t>(tot), st.room<uint32_t>(tot), st.room<uint64_t>(tot),
-                           nullptr};
-    st.flush();  // the inputs' span, if they lie in one crdt_host_alloc block
+    return std::max<uint64_t>(t, 1);
+}
+
+// Download merge outputs.  Default: at their capacity offsets, as the kernels
+// wrote them.  pack_batch_outputs: only the live entries, gathered on the
+// device at offsets computed on the device (pack_scan_kernel) -- an output
+// whose host arrays all lie in crdt_host_alloc blocks is written there by the
+// gather kernel itself (no copy call, no read-back: the call's one sync is its
+// last); any other is gathered on the device, and the totals of all such
+// outputs come back in ONE read-back before their copies.  keys[i] = false: an
+// exchange's second output sharing the first's key column.
+int fetch_outputs(crdt_ctx* ctx, Stager& st, int nout, const crdt_awset_out* const* h, const crdt_awset_out* d,
+                  const bool* keys, uint32_t n, uint32_t R, size_t slots) {
+    if (!ctx->pack_outputs) {
+        int rc = CRDT_OK;
+        for (int i = 0; i < nout && rc == CRDT_OK; ++i) rc = fetch_out(h[i], d[i], n, R, slots, ctx->stream, keys[i]);
+        return rc;
+    }
+    static const bool no_zc = std::getenv("CRDT_NO_ZERO_COPY") != nullptr;  // diagnostics: copies only
+    uint32_t* poff[2] = {nullptr, nullptr};
+    uint32_t* hoff[2] = {nullptr, nullptr};
+    OutView pk[2];
+    bool zc[2] = {false, false};
+    for (int i = 0; i < nout; ++i) {
+        poff[i] = st.room<uint32_t>((size_t)n + 1);
+        const uintptr_t ho = host_dev_addr(h[i]->offsets, ((size_t)n + 1) * 4),
+                        hc = host_dev_addr(h[i]->counts, (size_t)n * 4),
+                        hk = keys[i] ? host_dev_addr(h[i]->keys, slots * 8) : 1,
+                        ha = host_dev_addr(h[i]->actors, slots * 4), hcc = host_dev_addr(h[i]->counters, slots * 8),
+                        hv = host_dev_addr(h[i]->vv, (size_t)n * R * 8);
+        zc[i] = !no_zc && ho && hc && hk && ha && hcc && hv;
+        if (zc[i]) {
+            hoff[i] = reinterpret_cast<uint32_t*>(ho);
+            pk[i] = OutView{nullptr, reinterpret_cast<uint32_t*>(hc),
+                            keys[i] ? reinterpret_cast<uint64_t*>(hk) : nullptr, reinterpret_cast<uint32_t*>(ha),
+                            reinterpret_cast<uint64_t*>(hcc), reinterpret_cast<uint64_t*>(hv)};
+        } else {
+            pk[i] = OutView{nullptr, nullptr, keys[i] ? st.room<uint64_t>(slots) : nullptr, st.room<uint32_t>(slots),
+                            st.room<uint64_t>(slots), nullptr};
+        }
+    }
     if (st.rc != CRDT_OK) return st.rc;
-    rc = hip_err(launch_pack_out(view(&d), poff, n, view(&p), (uint32_t)ctx->n_cu, ctx->stream));
-    if (rc == CRDT_OK && keys) rc = get(h->keys, p.keys, tot, ctx->stream);
-    if (rc == CRDT_OK) rc = get(h->actors, p.actors, tot, ctx->stream);
-    if (rc == CRDT_OK) rc = get(h->counters, p.counters, tot, ctx->stream);
-    if (rc == CRDT_OK) rc = get(h->vv, d.vv, (size_t)n * R, ctx->stream);
+    int rc = CRDT_OK;
+    for (int i = 0; i < nout && rc == CRDT_OK; ++i) {
+        const uint32_t* gate = ctx->ws.as<uint32_t>(64);
+        rc = hip_err(launch_pack_scan(d[i].offsets, d[i].counts, n, poff[i], hoff[i], gate, ctx->stream));
+        if (rc == CRDT_OK)
+            rc = hip_err(launch_pack_out(view(&d[i]), poff[i], n, R, pk[i], gate, (uint32_t)ctx->n_cu, ctx->stream));
+    }
+    if (rc != CRDT_OK || (zc[0] && (nout < 2 || zc[1]))) return rc;
+    uint32_t tot[2] = {0, 0};
+    for (int i = 0; i < nout && rc == CRDT_OK; ++i)
+        if (!zc[i]) rc = get(&tot[i], poff[i] + n, 1, ctx->stream);
+    if (rc == CRDT_OK && hipStreamSynchronize(ctx->stream) != hipSuccess) rc = CRDT_E_HIP;
+    for (int i = 0; i < nout && rc == CRDT_OK; ++i) {
+        if (zc[i]) continue;
+        if (tot[i] > slots) return CRDT_E_CAPACITY;  // (the scan clamps to capacity: never)
+        rc = get(h[i]->offsets, poff[i], (size_t)n + 1, ctx->stream);
+        if (rc == CRDT_OK) rc = get(h[i]->counts, d[i].counts, n, ctx->stream);
+        if (rc == CRDT_OK && keys[i]) rc = get(h[i]->keys, pk[i].keys, tot[i], ctx->stream);
+        if (rc == CRDT_OK) rc = get(h[i]->actors, pk[i].actors, tot[i], ctx->stream);
+        if (rc == CRDT_OK) rc = get(h[i]->counters, pk[i].counters, tot[i], ctx->stream);
+        if (rc == CRDT_OK) rc = get(h[i]->vv, d[i].vv, (size_t)n * R, ctx->stream);
+    }
     return rc;
 }
 
@@ -1048,7 +1179,8 @@ int crdt_awset_sort_batch(crdt_ctx* ctx, const crdt_awset_batch* in, const crdt_
     int rc = set_device(ctx);
     if (rc != CRDT_OK) return rc;
     Stager st{ctx};
-    crdt_awset_batch di = stage_batch(st, in);
+    crdt_awset_batch di{};
+    st.plan([&] { di = stage_batch(st, in); });
     crdt_awset_out dout = stage_out(st, n, in->R, slots);
     st.flush();  // the inputs' span, if they lie in one crdt_host_alloc block
     if (st.rc != CRDT_OK) return st.rc;
@@ -1073,20 +1205,23 @@ int crdt_awset_apply_batch(crdt_ctx* ctx, const crdt_awset_batch* state, const c
     if (slots >= (1ull << 32) || tin + nops >= (1ull << 32)) return CRDT_E_INVALID;
     if ((rc = set_device(ctx)) != CRDT_OK) return rc;
     Stager st{ctx};
-    crdt_awset_batch ds = stage_batch(st, state);
+    crdt_awset_batch ds{};
     crdt_op_batch dops = *ops;
-    dops.op_off = st.put(ops->op_off, (size_t)n + 1);
-    dops.kind = st.put(ops->kind, nops);
-    dops.keys = st.put(ops->keys, nops);
-    dops.doc_actor = st.put(ops->doc_actor, n);
     crdt_tomb_batch dt{};
-    if (tombs) {
-        dt.offsets = st.put(tombs->offsets, (size_t)n + 1);
-        dt.counts = tombs->counts ? st.put(tombs->counts, n) : nullptr;
-        dt.keys = st.put(tombs->keys, tin);
-        dt.actors = st.put(tombs->actors, tin);
-        dt.counters = st.put(tombs->counters, tin);
-    }
+    st.plan([&] {
+        ds = stage_batch(st, state);
+        dops.op_off = st.put(ops->op_off, (size_t)n + 1);
+        dops.kind = st.put(ops->kind, nops);
+        dops.keys = st.put(ops->keys, nops);
+        dops.doc_actor = st.put(ops->doc_actor, n);
+        if (tombs) {
+            dt.offsets = st.put(tombs->offsets, (size_t)n + 1);
+            dt.counts = tombs->counts ? st.put(tombs->counts, n) : nullptr;
+            dt.keys = st.put(tombs->keys, tin);
+            dt.actors = st.put(tombs->actors, tin);
+            dt.counters = st.put(tombs->counters, tin);
+        }
+    });
     crdt_awset_out dout = stage_out(st, n, state->R, slots);
     crdt_tomb_out dto{};
     if (tomb_out) {
@@ -1112,6 +1247,12 @@ int crdt_awset_apply_batch(crdt_ctx* ctx, const crdt_awset_batch* state, const c
     return rc != CRDT_OK ? rc : sync;
 }
 
+// The merge calls below make one host sync each (their last): the inputs go up
+// (one copy of their span when they lie in one crdt_host_alloc block), the key
+// order is checked on the device, the merge's first kernel reads that verdict
+// (a batch out of order reaches no merge, Work::gate), and the outputs come
+// back (fetch_outputs: with pack_batch_outputs into page-locked outputs, by
+// the gather kernel itself).
 int crdt_awset_join_batch(crdt_ctx* ctx, const crdt_awset_batch* dst, const crdt_awset_batch* src,
                           const crdt_awset_out* out) {
     if (!ctx || !out_ptrs_ok(out)) return CRDT_E_INVALID;
@@ -1122,16 +1263,23 @@ int crdt_awset_join_batch(crdt_ctx* ctx, const crdt_awset_batch* dst, const crdt
     if ((uint64_t)dst->offsets[dst->n_docs] + src->offsets[src->n_docs] >= (1ull << 32)) return CRDT_E_INVALID;
     if ((rc = set_device(ctx)) != CRDT_OK) return rc;
     Stager st{ctx};
-    crdt_awset_batch dd = stage_batch(st, dst), ds = stage_batch(st, src);
+    crdt_awset_batch dd{}, ds{};
+    st.plan([&] {
+        dd = stage_batch(st, dst);
+        ds = stage_batch(st, src);
+    });
     const size_t slots = (size_t)dst->offsets[dst->n_docs] + src->offsets[src->n_docs];
     crdt_awset_out dout = stage_out(st, dst->n_docs, dst->R, slots);
     st.flush();  // the inputs' span, if they lie in one crdt_host_alloc block
     if (st.rc != CRDT_OK) return st.rc;
     rc = check_order(ctx, dd.offsets, dd.counts, dd.n_docs, dd.keys);
     if (rc == CRDT_OK) rc = check_order(ctx, ds.offsets, ds.counts, ds.n_docs, ds.keys);
-    rc = order_gate(ctx, rc);
-    if (rc == CRDT_OK) rc = crdt_awset_join_async(ctx, &dd, &ds, &dout, ctx->stream);
-    if (rc == CRDT_OK) rc = fetch_merge_out(ctx, st, out, dout, dst->n_docs, dst->R, slots);
+    ctx->call_tiles = host_tiles(ctx, dst, src);
+    if (rc == CRDT_OK) rc = gated(ctx, [&] { return crdt_awset_join_async(ctx, &dd, &ds, &dout, ctx->stream); });
+    const crdt_awset_out* hs[1] = {out};
+    const bool keys[1] = {true};
+    if (rc == CRDT_OK) rc = fetch_outputs(ctx, st, 1, hs, &dout, keys, dst->n_docs, dst->R, slots);
+    ctx->call_tiles = 0;
     const int sync = crdt_ctx_sync(ctx, ctx->stream);
     return rc != CRDT_OK ? rc : sync;
 }
@@ -1147,26 +1295,29 @@ int crdt_awset_exchange_batch(crdt_ctx* ctx, const crdt_awset_batch* a, const cr
     if ((rc = set_device(ctx)) != CRDT_OK) return rc;
     PhaseClock pc("exchange_batch");
     Stager st{ctx};
-    crdt_awset_batch da = stage_batch(st, a), db = stage_batch(st, b);
+    crdt_awset_batch da{}, db{};
+    st.plan([&] {
+        da = stage_batch(st, a);
+        db = stage_batch(st, b);
+    });
     const size_t slots = (size_t)a->offsets[a->n_docs] + b->offsets[b->n_docs];
-    crdt_awset_out o1 = stage_out(st, a->n_docs, a->R, slots);
-    crdt_awset_out o2 = stage_out(st, a->n_docs, a->R, slots);
+    crdt_awset_out o[2] = {stage_out(st, a->n_docs, a->R, slots), stage_out(st, a->n_docs, a->R, slots)};
     st.flush();  // the inputs' span, if they lie in one crdt_host_alloc block
     if (st.rc != CRDT_OK) return st.rc;
     // host outputs sharing one key column: one device column, written and fetched once
     const bool share = out_ab->keys == out_ba->keys;
-    if (share) o2.keys = o1.keys;
+    if (share) o[1].keys = o[0].keys;
     pc.mark("stage issued");
     rc = check_order(ctx, da.offsets, da.counts, da.n_docs, da.keys);
     if (rc == CRDT_OK) rc = check_order(ctx, db.offsets, db.counts, db.n_docs, db.keys);
-    rc = order_gate(ctx, rc);
-    pc.mark("order checked (a sync)");
-    if (rc == CRDT_OK) rc = crdt_awset_exchange_async(ctx, &da, &db, &o1, &o2, ctx->stream);
-    pc.mark("kernels issued");
-    if (rc == CRDT_OK) rc = fetch_merge_out(ctx, st, out_ab, o1, a->n_docs, a->R, slots);
-    pc.mark("fetch a<-b issued (after a sync)");
-    if (rc == CRDT_OK) rc = fetch_merge_out(ctx, st, out_ba, o2, a->n_docs, a->R, slots, !share);
-    pc.mark("fetch b<-a issued (after a sync)");
+    ctx->call_tiles = host_tiles(ctx, a, b);
+    if (rc == CRDT_OK) rc = gated(ctx, [&] { return crdt_awset_exchange_async(ctx, &da, &db, &o[0], &o[1], ctx->stream); });
+    pc.mark("order checks + kernels issued");
+    const crdt_awset_out* hs[2] = {out_ab, out_ba};
+    const bool keys[2] = {true, !share};
+    if (rc == CRDT_OK) rc = fetch_outputs(ctx, st, 2, hs, o, keys, a->n_docs, a->R, slots);
+    ctx->call_tiles = 0;
+    pc.mark("fetches issued");
     const int sync = crdt_ctx_sync(ctx, ctx->stream);
     pc.mark("synced");
     return rc != CRDT_OK ? rc : sync;
@@ -1185,32 +1336,36 @@ int crdt_awset_fold_batch(crdt_ctx* ctx, int mode, const crdt_awset_batch* dst, 
     if ((rc = set_device(ctx)) != CRDT_OK) return rc;
     if ((rc = reserve_scratch(ctx, total)) != CRDT_OK) return rc;
     Stager st{ctx};
-    crdt_awset_batch dd = stage_batch(st, dst);
+    crdt_awset_batch dd{};
     crdt_src_batch ds = *srcs;
     const size_t ne = srcs->entry_off[ns];
     const size_t nt = srcs->tomb_off ? srcs->tomb_off[ns] : 0;
-    ds.doc_srcs = st.put(srcs->doc_srcs, (size_t)srcs->n_docs + 1);
-    ds.src_actor = st.put(srcs->src_actor, ns);
-    ds.vv = st.put(srcs->vv, (size_t)ns * srcs->R);
-    ds.entry_off = st.put(srcs->entry_off, (size_t)ns + 1);
-    ds.keys = st.put(srcs->keys, ne);
-    ds.actors = st.put(srcs->actors, ne);
-    ds.counters = st.put(srcs->counters, ne);
-    if (srcs->tomb_off) {
-        ds.tomb_off = st.put(srcs->tomb_off, (size_t)ns + 1);
-        ds.tkeys = st.put(srcs->tkeys, nt);
-        ds.tactors = st.put(srcs->tactors, nt);
-        ds.tcounters = st.put(srcs->tcounters, nt);
-    }
+    st.plan([&] {
+        dd = stage_batch(st, dst);
+        ds.doc_srcs = st.put(srcs->doc_srcs, (size_t)srcs->n_docs + 1);
+        ds.src_actor = st.put(srcs->src_actor, ns);
+        ds.vv = st.put(srcs->vv, (size_t)ns * srcs->R);
+        ds.entry_off = st.put(srcs->entry_off, (size_t)ns + 1);
+        ds.keys = st.put(srcs->keys, ne);
+        ds.actors = st.put(srcs->actors, ne);
+        ds.counters = st.put(srcs->counters, ne);
+        if (srcs->tomb_off) {
+            ds.tomb_off = st.put(srcs->tomb_off, (size_t)ns + 1);
+            ds.tkeys = st.put(srcs->tkeys, nt);
+            ds.tactors = st.put(srcs->tactors, nt);
+            ds.tcounters = st.put(srcs->tcounters, nt);
+        }
+    });
     crdt_awset_out dout = stage_out(st, dst->n_docs, dst->R, total);
     st.flush();  // the inputs' span, if they lie in one crdt_host_alloc block
     if (st.rc != CRDT_OK) return st.rc;
     rc = check_order(ctx, dd.offsets, dd.counts, dd.n_docs, dd.keys);
     if (rc == CRDT_OK) rc = check_order(ctx, ds.entry_off, nullptr, ns, ds.keys);
     if (rc == CRDT_OK && srcs->tomb_off) rc = check_order(ctx, ds.tomb_off, nullptr, ns, ds.tkeys);
-    rc = order_gate(ctx, rc);
-    if (rc == CRDT_OK) rc = crdt_awset_fold_async(ctx, mode, &dd, &ds, &dout, ctx->stream);
-    if (rc == CRDT_OK) rc = fetch_merge_out(ctx, st, out, dout, dst->n_docs, dst->R, total);
+    if (rc == CRDT_OK) rc = gated(ctx, [&] { return crdt_awset_fold_async(ctx, mode, &dd, &ds, &dout, ctx->stream); });
+    const crdt_awset_out* hs[1] = {out};
+    const bool keys[1] = {true};
+    if (rc == CRDT_OK) rc = fetch_outputs(ctx, st, 1, hs, &dout, keys, dst->n_docs, dst->R, total);
     const int sync = crdt_ctx_sync(ctx, ctx->stream);
     return rc != CRDT_OK ? rc : sync;
 }

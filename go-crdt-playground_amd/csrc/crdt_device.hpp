@@ -74,7 +74,17 @@ struct Work {
     uint32_t* chunk_ctr;   // [8] dispenser shards (the tile path's, TileWork::head)
     uint32_t* defer;       // [n_docs] folds: documents the lean pass leaves to the general one
     uint32_t* defer_count; // number of deferred documents
+    // Host-path calls (crdt_awset_*_batch): the status word their device key-order
+    // checks (pack.hip) wrote.  The first kernel of the merge returns at once when
+    // it holds kErrUnsorted, so a batch whose keys are out of order never reaches
+    // a merge and no host read-back gates the launch.  NULL: no gate.
+    const uint32_t* gate;
 };
+
+// The merge's first kernel: false when the host path's order checks failed (Work::gate).
+__device__ __forceinline__ bool gate_open(const Work& wk) {
+    return !wk.gate || (*wk.gate & kErrUnsorted) == 0u;
+}
 
 // Batched local ops (apply.hip): the op lists, tombstones in and out.
 struct ApplyOps {
@@ -101,22 +111,30 @@ struct TombOut {
     uint64_t* counters;
 };
 
-// Workspace of the large-document tile path (tile.hip).
+// Workspace of the large-document tile path (tile.hip).  A call's tiles are
+// numbered 0 .. total-1 over all its documents and run in passes of at most
+// `cap` tiles (pass p: tiles [p*cap, p*cap + cap)); the per-tile arrays hold
+// one pass, indexed by the tile's position within it.
 struct TileWork {
-    uint4* desc;          // [cap] {doc, tile index in doc, i0, j0}
+    uint4* desc;          // [cap + 1] {doc, tile index in doc, i0, j0}; + the next pass's first tile
     uint4* geo;           // [2*cap] per-tile geometry (tile.hip, tile_geo_kernel)
     uint64_t* flags;      // [cap] look-back words
     uint32_t* slot_incl;  // [n_docs] inclusive tile count within the slot's run
     uint32_t* run;        // [ceil(n_docs/kRun)] run sums -> exclusive prefixes
-    uint32_t* total;      // workspace word: tiles of this call
+    uint32_t* total;      // workspace word: tiles of this call (every pass)
     uint32_t* head;       // workspace words [shards]: tile dispensers (tile.hip, tile_take)
-    uint32_t* fallback;   // workspace word: 1 = tiles exceed cap, block kernel runs
+    uint32_t* fallback;   // workspace word: 1 = tiles exceed passes x cap, block kernel runs
+    uint32_t* carry;      // workspace words [2]: survivors a document's tiles of the previous pass
+                          // placed, for its tiles in this pass (indexed by pass parity)
     uint32_t cap;
     uint32_t tile;   // merged positions per tile (= the tile kernel's NT * IPT)
     uint32_t shape;  // tile kernel shape (tile.hip, tile_positions)
     uint32_t nt_stores;  // non-temporal output stores ("join_tile_nt_stores")
     uint32_t split_bpc;  // tile_split_kernel workgroups per CU ("join_tile_split_blocks_per_cu")
     uint32_t shards;     // tile dispenser words, 1 or 8 ("join_tile_dispensers")
+    uint32_t pass;       // the pass this launch runs
+    uint32_t passes;     // passes the host launches (more tiles than passes x cap: fallback)
+    uint32_t covered;    // 1: passes x cap holds every tile the call can have (no block-kernel fallback launched)
 };
 
 // ---- slab order of a grid's blocks.  A streaming kernel whose concurrently

@@ -99,6 +99,13 @@ namespace crdt {
 #ifndef CRDT_FOLD_NO_STORES
 #define CRDT_FOLD_NO_STORES 0
 #endif
+// diagnostic bounds (timing builds only): no per-document fold / no loads after the first document
+#ifndef CRDT_FOLD_DIAG_NOCOMPUTE
+#define CRDT_FOLD_DIAG_NOCOMPUTE 0
+#endif
+#ifndef CRDT_FOLD_DIAG_NOLOAD
+#define CRDT_FOLD_DIAG_NOLOAD 0
+#endif
 // CRDT_FOLD_PAD_STORES (with CRDT_FOLD_STAGE_STORES 1, diagnostic): each array's
 // staged stores run on to the end of the last survivor's cache line, within
 // the document's output capacity (slack past the live count is unspecified),
@@ -127,6 +134,21 @@ namespace crdt {
 #ifndef CRDT_FOLD_LDS_PAD
 #define CRDT_FOLD_LDS_PAD 0
 #endif
+// CRDT_FOLD_GLOBAL_PTAB: the PTAB prefetch's tuple loads through global-address-
+// space pointers (global_load) instead of generic ones (flat_load, which also
+// counts in lgkmcnt: every LDS wait of the fold then waited for the prefetch).
+#ifndef CRDT_FOLD_GLOBAL_PTAB
+#define CRDT_FOLD_GLOBAL_PTAB 1
+#endif
+// CRDT_FOLD_TOMB_TAB: the delta classify's "re-added in the same source" check
+// (awset-delta_test.go:93-102) through a per-low-key-byte step bitmap, searching
+// the source's entries only on a possible hit (see the classify pass).
+#ifndef CRDT_FOLD_TOMB_TAB
+#define CRDT_FOLD_TOMB_TAB 1
+#endif
+// pointer to global (address space 1) memory
+template <typename T>
+using gptr = const T __attribute__((address_space(1)))*;
 #ifndef CRDT_FOLD_PAD_VALU
 #define CRDT_FOLD_PAD_VALU 0
 #endif
@@ -933,7 +955,7 @@ __global__ __launch_bounds__(fold_waves<DELTA>() * 64) __attribute__((amdgpu_wav
                                       n_docs)
                                 : n_docs;
     const uint32_t first = uniform((blockIdx.x * fold_waves<DELTA>() + w) * (uint32_t)K);
-    if (first >= n_run) return;
+    if (first >= n_run || !gate_open(wk)) return;  // (a closed gate: nothing deferred or pushed either)
     const uint32_t cnt = min((uint32_t)K, n_run - first);
 
     // ---- metadata of the run: lane i <= cnt describes document first + i (LIST:
@@ -1051,9 +1073,19 @@ __global__ __launch_bounds__(fold_waves<DELTA>() * 64) __attribute__((amdgpu_wav
                 i = i < q.N ? i : q.N - 1u;
                 const uint32_t r4 = (i >= q.n ? 4u : 0u) + (i >= nE ? 4u : 0u);
                 const uint64_t kb = ptab[r4], cb = ptab[r4 + 1], ab = ptab[r4 + 2];
+#if CRDT_FOLD_GLOBAL_PTAB
+                // Global (not generic) loads: a FLAT load also counts in lgkmcnt, so
+                // every LDS wait of the current document's fold -- the first comes
+                // right after this prefetch -- would wait for the next document's
+                // HBM loads too, and the prefetch would overlap nothing.
+                P.k[c] = __builtin_nontemporal_load(reinterpret_cast<gptr<uint64_t>>(kb) + i);
+                P.a[c] = __builtin_nontemporal_load(reinterpret_cast<gptr<uint32_t>>(ab) + i);
+                P.c[c] = __builtin_nontemporal_load(reinterpret_cast<gptr<uint64_t>>(cb) + i);
+#else
                 P.k[c] = __builtin_nontemporal_load(reinterpret_cast<const uint64_t*>(kb) + i);
                 P.a[c] = __builtin_nontemporal_load(reinterpret_cast<const uint32_t*>(ab) + i);
                 P.c[c] = __builtin_nontemporal_load(reinterpret_cast<const uint64_t*>(cb) + i);
+#endif
             }
         }
         } else {
@@ -1184,14 +1216,17 @@ __global__ __launch_bounds__(fold_waves<DELTA>() * 64) __attribute__((amdgpu_wav
                     if ((uint32_t)c * 64u < msR && i < msR) m.svv[i] = P.sv[c];
                 }
             }
+            // (CRDT_FOLD_DIAG_NOLOAD: the offsets held are the run's first document's)
+            const uint32_t e0 = CRDT_FOLD_DIAG_NOLOAD ? rl(P.eo, 0) : cur.e0;
+            const uint32_t t0 = CRDT_FOLD_DIAG_NOLOAD ? rl(P.to, 0) : cur.t0;
             const uint32_t nso = from_next_lane(LEAN ? 0u : rl(P.eo2, 0), P.eo);
-            soffv = nso - cur.e0;
+            soffv = nso - e0;
             // per-source words of every lane (MCAP = 64: lanes past ms write words no step reads)
-            m.soff[lane] = P.eo - cur.e0;
-            if (cur.ms >= 64 && lane == 0) m.soff[64] = P.eo2 - cur.e0;
+            m.soff[lane] = P.eo - e0;
+            if (cur.ms >= 64 && lane == 0) m.soff[64] = P.eo2 - e0;
             if (tombs) {
                 const uint32_t nto = from_next_lane(LEAN ? 0u : rl(P.to2, 0), P.to);
-                toffv = nto - cur.t0;
+                toffv = nto - t0;
             }
             m.sact[lane] = P.act;
             reinterpret_cast<uint32_t*>(m.smark)[lane & (Smem::NCAP / 4 - 1)] = 0u;
@@ -1209,7 +1244,9 @@ __global__ __launch_bounds__(fold_waves<DELTA>() * 64) __attribute__((amdgpu_wav
         wave_sync();
         STAMP(0)
         // ---- issue document k+1's loads; they fly while document k is folded
-        if (k + 1 < cnt) {
+        // (CRDT_FOLD_DIAG_NOLOAD, diagnostic: none -- every document of the run folds
+        // the first one's tuples, which in configs 3 and 5 have the same shape)
+        if (k + 1 < cnt && !CRDT_FOLD_DIAG_NOLOAD) {
             const DocMeta nxt = meta(k + 1);
             STAMP(12)
             if (!nxt.big) prefetch(P, nxt);
@@ -1221,7 +1258,26 @@ __global__ __launch_bounds__(fold_waves<DELTA>() * 64) __attribute__((amdgpu_wav
         uint32_t U = 0;  // survivors
         bool deferred = false;  // LEAN: the document is left to the general kernel
         Emit<NCH> em;
+#if CRDT_FOLD_DIAG_NOCOMPUTE
+        // diagnostic bound (tools/fold_probe timing builds): no fold at all -- the
+        // document's own entries written back as its survivors (memory traffic and
+        // the pipeline, without the per-document chain)
         if (!cur.big) {
+#pragma unroll
+            for (int q = 0; q < NCH; ++q) {
+                const uint32_t i = q * 64u + lane;
+                em.k[q] = m.tk[i];
+                em.a[q] = m.ta[i];
+                em.c[q] = m.tc[i];
+                em.off[q] = i < cur.n ? i : kOOB;
+            }
+            U = cur.n;
+            vfin = vreg;
+        }
+        if (false) {
+#else
+        if (!cur.big) {
+#endif
             const uint32_t n = cur.n, E = cur.E, N = cur.N, ms = cur.ms;
             // schedule: U_j, one lane per actor
             uint64_t v = vreg;
@@ -1304,6 +1360,19 @@ __global__ __launch_bounds__(fold_waves<DELTA>() * 64) __attribute__((amdgpu_wav
                 cmax = (uint32_t)__builtin_amdgcn_readlane((int)cmax, 63);  // ... whose last lane has the maximum
             }
             STAMP(11)
+            // CRDT_FOLD_TOMB_TAB: est[key & 255] = the steps (< 32) with an entry of that
+            // low key byte, so a tombstone whose step bit is clear was not re-added in
+            // its source (effective) without the binary search below; a set bit (the
+            // key, or another one with the same low byte) still searches.  Scratch:
+            // stag onwards, dead until the keep phase / the walk.
+            const bool tab = CRDT_FOLD_TOMB_TAB && DELTA && cur.X != 0 && ms <= 32;
+            uint32_t* est = reinterpret_cast<uint32_t*>(m.stag);
+            static_assert(offsetof(Smem, dbase) + sizeof(m.dbase) - offsetof(Smem, stag) >= 1024,
+                          "fold: step table space");
+            if (tab) {
+                reinterpret_cast<uint4*>(est)[lane] = make_uint4(0u, 0u, 0u, 0u);
+                wave_sync();
+            }
             uint64_t key[NCH];
             uint32_t flag = 0, perr = 0;  // flag bit c: changed entry / effective tombstone
             uint64_t me = 0, mt = 0;      // steps of this lane's changed entries / effective tombstones
@@ -1359,7 +1428,13 @@ __global__ __launch_bounds__(fold_waves<DELTA>() * 64) __attribute__((amdgpu_wav
                         f = !(a < R && m.vs[j * R + a] >= cc);
                         me |= f ? 1ull << j : 0ull;
                     }
-                    if (DELTA && isT[c]) {
+                    // (before the tombstones' reads: this chunk's and every earlier one's
+                    // entries are in the table when a tombstone of the chunk looks)
+                    if (tab && isE[c]) atomicOr(&est[(uint32_t)key[c] & 255u], 1u << j);
+                    if (DELTA && isT[c] && tab && !((est[(uint32_t)key[c] & 255u] >> j) & 1u)) {
+                        f = true;  // no entry of this key in source j: effective (:93-102)
+                        mt |= 1ull << j;
+                    } else if (DELTA && isT[c]) {
                         // effective: not re-added in the same source (:93-102)
                         const uint32_t lo = n + m.soff[j], len = m.soff[j + 1] - m.soff[j];
                         uint32_t pos = 0;

@@ -302,7 +302,7 @@ __global__ __launch_bounds__(WAVES * 64) CRDT_JOIN_WPE_ATTR void join_wave_kerne
     uint32_t err = 0;
 
     const uint32_t chunk = slab_chunk(slabs, blockIdx.x);
-    if (chunk == 0xFFFFFFFFu) return;
+    if (chunk == 0xFFFFFFFFu || !gate_open(wk)) return;  // (a closed gate: nothing reaches the worklist either)
     const uint32_t first = uniform(chunk * (WAVES * K) + w);
     if (first >= n_docs) return;
     const uint32_t cnt = min((uint32_t)K, (n_docs - first + WAVES - 1) / WAVES);
@@ -493,7 +493,7 @@ hipError_t launch_join(const BatchView& dst, const BatchView& src, const OutView
     const uint32_t* gate = nullptr;
     if (tw) {
         e = launch_join_tiles(dst, src, out, out2, wk, *tw, n_cu, stream);
-        if (e != hipSuccess) return e;
+        if (e != hipSuccess || tw->covered) return e;  // covered: the passes hold every tile, no fallback
         gate = tw->fallback;
     }
     hipLaunchKernelGGL((join_block_kernel<kBlockNT, kBlockIPT>), dim3(block_grid), dim3(kBlockNT), 0, stream, dst,

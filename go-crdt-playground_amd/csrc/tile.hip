@@ -86,11 +86,25 @@ __global__ __launch_bounds__(NT) void tile_scan_kernel(uint32_t n_docs, Work wk,
         if (r < n_runs) tw.run[r] = (uint32_t)min<uint64_t>(carry + ex, 0xFFFFFFFFull);
         carry += tot;
     }
-    if (threadIdx.x == 0) {
-        const bool over = carry > tw.cap;
+    if (threadIdx.x == 0) {  // more tiles than the launched passes hold: the block kernel takes the worklist
+        const bool over = carry > (uint64_t)tw.cap * tw.passes;
         *tw.fallback = over ? 1u : 0u;
         *tw.total = over ? 0u : (uint32_t)carry;
     }
+}
+
+// This launch's pass: tiles [base, base + count) of the call's `total`.
+struct TilePass {
+    uint32_t base, count;
+};
+__device__ __forceinline__ TilePass tile_pass(const TileWork& tw, uint32_t total) {
+    const uint64_t b = (uint64_t)tw.pass * tw.cap;
+    TilePass p{0u, 0u};
+    if (b < total) {
+        p.base = (uint32_t)b;
+        p.count = min(tw.cap, total - p.base);
+    }
+    return p;
 }
 
 // Merge-path split at diagonal k whose answer is known to lie in [lo, hi]
@@ -157,14 +171,20 @@ __device__ __forceinline__ uint32_t merge_path_gallop(const uint64_t* dk, const 
 // so the deep levels of the search -- a line fetched per level -- are fewer.
 constexpr uint32_t kSplitRun = 4;
 
+// Tiles of one pass, plus the first tile of the next pass: its split is where
+// this pass's last tile ends (tile_geo_kernel).
 template <int NT>
 __global__ __launch_bounds__(NT) void tile_split_kernel(BatchView A, BatchView B, Work wk, TileWork tw) {
     const uint32_t total = *tw.total;
+    const TilePass ps = tile_pass(tw, total);
+    if (ps.count == 0) return;
+    const uint32_t n_split = min(ps.count + 1u, total - ps.base);
     const uint32_t total_slots = work_total(wk, A.n_docs);
     const uint32_t n_runs = (total_slots + kRun - 1) / kRun;
     uint32_t pd = 0xFFFFFFFFu, pt = 0, pi = 0;  // this thread's previous tile: document, index, split
-    for (uint32_t g0 = (blockIdx.x * NT + threadIdx.x) * kSplitRun; g0 < total; g0 += gridDim.x * NT * kSplitRun)
-    for (uint32_t g = g0; g < min(g0 + kSplitRun, total); ++g) {
+    for (uint32_t l0 = (blockIdx.x * NT + threadIdx.x) * kSplitRun; l0 < n_split; l0 += gridDim.x * NT * kSplitRun)
+    for (uint32_t l = l0; l < min(l0 + kSplitRun, n_split); ++l) {
+        const uint32_t g = ps.base + l;  // the call's tile number
         // run: last r with run[r] <= g (run prefixes strictly increase: every slot has >= 1 tile)
         uint32_t lo = 0, hi = n_runs;
         while (hi - lo > 1) {
@@ -210,8 +230,8 @@ __global__ __launch_bounds__(NT) void tile_split_kernel(BatchView A, BatchView B
         pd = d;
         pt = t;
         pi = i0;
-        tw.desc[g] = make_uint4(d, t, i0, j0);
-        tw.flags[g] = 0ull;
+        tw.desc[l] = make_uint4(d, t, i0, j0);
+        if (l < ps.count) tw.flags[l] = 0ull;
     }
 }
 
@@ -293,6 +313,7 @@ __device__ __forceinline__ uint32_t look_back(uint64_t* flags, uint32_t g, uint3
 struct TileGeo {
     uint32_t d, t, ga, gb, nA, nB, obase;  // ga/gb: absolute slot of the tile's first dst/src element
     bool last, has_next, has_prev, bad;
+    bool cont_in, cont_out;  // the document continues from the previous pass / into the next
 };
 
 // A tile's geometry record sits with those of its dispenser shard (tile_take):
@@ -307,18 +328,29 @@ __device__ __forceinline__ size_t geo_slot(const TileWork& tw, uint32_t g) {
 // Per-tile geometry, precomputed once per call (tile_geo_kernel) so that a
 // workgroup's dependent chain per tile is dispense -> one 32-byte record ->
 // data loads.
+// Flags of a tile's geometry record (r1.z): the document's last tile, a src
+// element past the tile, a dst element before it; the first tile of this pass
+// continuing a document of the previous pass (its tiles there placed
+// tw.carry[pass & 1] survivors), the last tile of this pass whose document
+// continues in the next (it hands on its inclusive count).
+constexpr uint32_t kGeoLast = 1u, kGeoNext = 2u, kGeoPrev = 4u, kGeoContIn = 8u, kGeoContOut = 16u;
+
 __global__ __launch_bounds__(256) void tile_geo_kernel(BatchView A, BatchView B, TileWork tw) {
     const uint32_t total = *tw.total;
-    for (uint32_t g = blockIdx.x * 256 + threadIdx.x; g < total; g += gridDim.x * 256) {
-        const uint4 ds = tw.desc[g];
+    const TilePass ps = tile_pass(tw, total);
+    // this pass's dispensers start at 0 (the previous pass's tile kernel, which
+    // advanced them, has finished; pass 0's were zeroed with the call's counters)
+    if (tw.pass && blockIdx.x == 0 && threadIdx.x < tw.shards) tw.head[threadIdx.x] = 0u;
+    for (uint32_t l = blockIdx.x * 256 + threadIdx.x; l < ps.count; l += gridDim.x * 256) {
+        const uint4 ds = tw.desc[l];
         const uint32_t d = ds.x, t = ds.y, i0 = ds.z, j0 = ds.w;
-        uint4 r0 = make_uint4(d, t, 0u, 0u), r1 = make_uint4(0u, 0u, 1u, 0u);
+        uint4 r0 = make_uint4(d, t, 0u, 0u), r1 = make_uint4(0u, 0u, kGeoLast, 0u);
         if (d < A.n_docs) {
             const uint32_t nd = live_count(A.offsets, A.counts, d), ns = live_count(B.offsets, B.counts, d);
             const uint32_t aoff = A.offsets[d], boff = B.offsets[d];
-            uint32_t i1 = nd, j1 = ns, last = 1u;
-            if (g + 1 < total) {
-                const uint4 nx = tw.desc[g + 1];
+            uint32_t i1 = nd, j1 = ns, last = kGeoLast;
+            if (ps.base + l + 1 < total) {  // (desc[count] is the next pass's first tile)
+                const uint4 nx = tw.desc[l + 1];
                 if (nx.x == d && nx.y == t + 1) {
                     i1 = nx.z;
                     j1 = nx.w;
@@ -329,10 +361,11 @@ __global__ __launch_bounds__(256) void tile_geo_kernel(BatchView A, BatchView B,
             r0.w = boff + j0;
             r1.x = i1 - i0;
             r1.y = j1 - j0;
-            r1.z = last | (j1 < ns ? 2u : 0u) | (i0 > 0 ? 4u : 0u);
+            r1.z = last | (j1 < ns ? kGeoNext : 0u) | (i0 > 0 ? kGeoPrev : 0u) |
+                   ((l == 0 && t > 0) ? kGeoContIn : 0u) | ((l + 1 == ps.count && !last) ? kGeoContOut : 0u);
             r1.w = aoff + boff;
         }
-        const size_t at = geo_slot(tw, g);
+        const size_t at = geo_slot(tw, l);
         tw.geo[2 * at] = r0;
         tw.geo[2 * at + 1] = r1;
     }
@@ -348,12 +381,14 @@ __device__ __forceinline__ TileGeo tile_geo(const BatchView& A, const TileWork& 
     x.gb = r0.w;
     x.nA = r1.x;
     x.nB = r1.y;
-    x.last = (r1.z & 1u) != 0;
-    x.has_next = (r1.z & 2u) != 0;
-    x.has_prev = (r1.z & 4u) != 0;
+    x.last = (r1.z & kGeoLast) != 0;
+    x.has_next = (r1.z & kGeoNext) != 0;
+    x.has_prev = (r1.z & kGeoPrev) != 0;
+    x.cont_in = (r1.z & kGeoContIn) != 0;
+    x.cont_out = (r1.z & kGeoContOut) != 0;
     x.obase = r1.w;
     x.bad = x.d >= A.n_docs;  // not a document of this call: never dereferenced
-    if (x.bad) x.nA = x.nB = 0, x.has_next = x.has_prev = false;
+    if (x.bad) x.nA = x.nB = 0, x.has_next = x.has_prev = x.cont_in = x.cont_out = false;
     return x;
 }
 
@@ -575,7 +610,9 @@ __global__ __launch_bounds__(NT) void join_tile_kernel(BatchView A, BatchView B,
     __shared__ TileSmem<NT, IPT> sm;
     const uint32_t tid = threadIdx.x, lane = tid & 63;
     const uint32_t R = A.R;
-    const uint32_t total = *tw.total;
+    const uint32_t total = tile_pass(tw, *tw.total).count;  // this pass's tiles, numbered from 0
+    if (total == 0) return;  // a pass past the call's tiles
+    const uint32_t carry_in = tw.pass ? tw.carry[tw.pass & 1u] : 0u;
     uint32_t err = 0;
     TileRegs<IPT> rg;
     STAMP_DECL
@@ -599,13 +636,15 @@ __global__ __launch_bounds__(NT) void join_tile_kernel(BatchView A, BatchView B,
                     atomicOr(wk.status, kErrWorkspace);
                     flag_store(tw.flags + g, kFlagInc);
                 }
-            } else if (cur.t == 0) {
-                if (lane == 0) flag_store(tw.flags + g, kFlagInc | agg);
+            } else if (cur.t == 0 || cur.cont_in) {  // a document's first tile (in this pass): inclusive at once
+                prefix = cur.t == 0 ? 0u : carry_in;
+                if (lane == 0) flag_store(tw.flags + g, kFlagInc | (prefix + agg));
             } else {
                 if (lane == 0) flag_store(tw.flags + g, kFlagAgg | agg);
-                prefix = look_back(tw.flags, g, cur.t, lane);
+                prefix = look_back(tw.flags, g, min(cur.t, g), lane);
                 if (lane == 0) flag_store(tw.flags + g, kFlagInc | (prefix + agg));
             }
+            if (cur.cont_out && lane == 0) tw.carry[(tw.pass + 1u) & 1u] = prefix + agg;  // for the next pass
             // nothing of this tile waits on another workgroup any more: take the
             // next tile now (a tile taken earlier would be held while this one's
             // look-back waits, and its successors would wait on that in turn)
@@ -644,13 +683,15 @@ __global__ __launch_bounds__(NT) void join_tile_kernel(BatchView A, BatchView B,
 // every walk ends (each tile's aggregate is published without waiting, and
 // tile 0 of a document publishes its inclusive count).
 template <int NT, int IPT, bool EXCH, bool NTS, bool ALIGN>
-__global__ __launch_bounds__(NT) void join_tile_pipe_kernel(BatchView A, BatchView B, OutView o1, OutView o2,
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(6))) void join_tile_pipe_kernel(BatchView A, BatchView B, OutView o1, OutView o2,
                                                             TileWork tw, Work wk) {
     __shared__ TileSmem<NT, IPT> sm[2];
     __shared__ uint32_t word[2];
     const uint32_t tid = threadIdx.x, lane = tid & 63;
     const uint32_t R = A.R;
-    const uint32_t total = *tw.total;
+    const uint32_t total = tile_pass(tw, *tw.total).count;  // this pass's tiles, numbered from 0
+    if (total == 0) return;  // a pass past the call's tiles
+    const uint32_t carry_in = tw.pass ? tw.carry[tw.pass & 1u] : 0u;
     uint32_t err = 0;
     TileRegs<IPT> rg;
     STAMP_DECL
@@ -672,14 +713,18 @@ __global__ __launch_bounds__(NT) void join_tile_pipe_kernel(BatchView A, BatchVi
     auto resolve0 = [&](uint32_t& prefix0, uint32_t& g2) {
         if (tid < 64) {
             uint32_t p0 = 0;
-            if (g0 < total && !x0.bad && x0.t != 0) {
+            const bool live0 = g0 < total && !x0.bad;
+            if (live0 && x0.cont_in) {
+                p0 = carry_in;  // (published inclusive by publish1)
+            } else if (live0 && x0.t != 0) {
 #ifdef CRDT_STAMPS
-                p0 = look_back(tw.flags, g0, x0.t, lane, st_acc + 8);
+                p0 = look_back(tw.flags, g0, min(x0.t, g0), lane, st_acc + 8);
 #else
-                p0 = look_back(tw.flags, g0, x0.t, lane);
+                p0 = look_back(tw.flags, g0, min(x0.t, g0), lane);
 #endif
                 if (lane == 0) flag_store(tw.flags + g0, kFlagInc | (p0 + agg0));
             }
+            if (live0 && x0.cont_out && lane == 0) tw.carry[(tw.pass + 1u) & 1u] = p0 + agg0;  // for the next pass
             if (lane == 0) {
                 word[1] = p0;
                 word[0] = tile_take(tw);
@@ -694,6 +739,8 @@ __global__ __launch_bounds__(NT) void join_tile_pipe_kernel(BatchView A, BatchVi
             if (x1.bad) {
                 atomicOr(wk.status, kErrWorkspace);
                 flag_store(tw.flags + g1, kFlagInc);
+            } else if (x1.cont_in) {  // first tile of this pass, its document begun in the previous one
+                flag_store(tw.flags + g1, kFlagInc | (carry_in + agg1));
             } else {
                 flag_store(tw.flags + g1, (x1.t == 0 ? kFlagInc : kFlagAgg) | agg1);
             }
@@ -808,17 +855,10 @@ uint32_t tile_positions(uint32_t shape) {
 
 // Launch the tile path for the worklist the wave kernel filled.  n_cu sizes the
 // persistent grid.  out2 != nullptr: exchange.
-hipError_t launch_join_tiles(const BatchView& A, const BatchView& B, const OutView& o1, const OutView* o2,
-                             const Work& wk, const TileWork& tw, uint32_t n_cu, hipStream_t stream) {
-    const uint32_t n_runs = (A.n_docs + kRun - 1) / kRun;
-    hipLaunchKernelGGL((tile_count_kernel<256>), dim3(min(n_runs, 2048u)), dim3(256), 0, stream, A, B, wk, tw);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL((tile_scan_kernel<1024>), dim3(1), dim3(1024), 0, stream, A.n_docs, wk, tw);
-    e = hipGetLastError();
-    if (e != hipSuccess) return e;
+static hipError_t launch_tile_pass(const BatchView& A, const BatchView& B, const OutView& o1, const OutView* o2,
+                                   const Work& wk, const TileWork& tw, uint32_t n_cu, hipStream_t stream) {
     hipLaunchKernelGGL((tile_split_kernel<256>), dim3(n_cu * tw.split_bpc), dim3(256), 0, stream, A, B, wk, tw);
-    e = hipGetLastError();
+    hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(tile_geo_kernel, dim3(n_cu * 4), dim3(256), 0, stream, A, B, tw);
     e = hipGetLastError();
@@ -836,6 +876,30 @@ hipError_t launch_join_tiles(const BatchView& A, const BatchView& B, const OutVi
         case 10: return launch_tile_pipe<256, 2, true>(A, B, o1, o2, wk, tw, n_cu, stream);
         default: return launch_tile_kernel<512, 4>(A, B, o1, o2, wk, tw, n_cu, stream);
     }
+}
+
+// The plan, then tw.passes passes of at most tw.cap tiles each (split, geometry,
+// tile kernel): a call's tiles need no workspace beyond one pass, and a pass
+// may end inside a document (tw.carry hands its placed count on).  Passes past
+// the call's tiles return at once; more tiles than tw.passes * tw.cap set
+// tw.fallback and leave the worklist to the block kernel.
+hipError_t launch_join_tiles(const BatchView& A, const BatchView& B, const OutView& o1, const OutView* o2,
+                             const Work& wk, const TileWork& tw_in, uint32_t n_cu, hipStream_t stream) {
+    TileWork tw = tw_in;
+    // every dispenser shard needs a resident workgroup (tile_take); the
+    // persistent grid has n_cu x occupancy >= n_cu of them
+    tw.shards = max(1u, min(tw.shards, n_cu));
+    const uint32_t n_runs = (A.n_docs + kRun - 1) / kRun;
+    hipLaunchKernelGGL((tile_count_kernel<256>), dim3(min(n_runs, 2048u)), dim3(256), 0, stream, A, B, wk, tw);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL((tile_scan_kernel<1024>), dim3(1), dim3(1024), 0, stream, A.n_docs, wk, tw);
+    e = hipGetLastError();
+    for (uint32_t p = 0; p < tw.passes && e == hipSuccess; ++p) {
+        tw.pass = p;
+        e = launch_tile_pass(A, B, o1, o2, wk, tw, n_cu, stream);
+    }
+    return e;
 }
 
 }  // namespace crdt

@@ -12,12 +12,15 @@
 // keys, string keys of 12-16 bytes), n docs (default 65,536).  One untimed
 // call on a copy of the states first (it sizes the page-locked staging and the
 // host scratch, which a long-running caller keeps).  Both the GPU path and the
-// CPU reference merge run on copy-constructed maps of the same states.
+// CPU reference merge run on copy-constructed maps of the same states, and
+// every document of both directions is compared between them afterwards
+// (sample_docs_checked = docs), plus 64 documents against single Merge calls.
 // Prints one JSON object.  GPU box only.
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../go-crdt-playground_amd/host/crdt.hpp"
@@ -125,20 +128,32 @@ int main(int argc, char** argv) {
             }
         });
         cpu_s = std::chrono::duration<double>(clk::now() - c0).count();
-        for (size_t i = 0; i < sample.size(); ++i) {
-            const size_t d = sample[i];
-            bad += CA[d].entries != A[d].entries || CA[d].versionVector != A[d].versionVector;
-            bad += CB[d].entries != B[d].entries || CB[d].versionVector != B[d].versionVector;
-        }
     }
+    // every document of both directions against the reference merge on the
+    // same states (untimed; one thread per document range)
+    std::vector<size_t> bad_of(detail::host_threads() + 1, 0);
+    {
+        std::vector<std::thread> pool;
+        const size_t t = bad_of.size(), chunk = (n + t - 1) / t;
+        for (size_t i = 0; i < t; ++i)
+            pool.emplace_back([&, i] {
+                for (size_t d = i * chunk; d < std::min(n, (i + 1) * chunk); ++d) {
+                    bad_of[i] += CA[d].entries != A[d].entries || CA[d].versionVector != A[d].versionVector;
+                    bad_of[i] += CB[d].entries != B[d].entries || CB[d].versionVector != B[d].versionVector;
+                }
+            });
+        for (auto& th : pool) th.join();
+    }
+    for (size_t b : bad_of) bad += b;
     const double merges = 2.0 * n;
     printf("{\"docs\": %zu, \"entries_per_replica\": %d, \"out_entries_per_doc\": %.2f, \"pack_s\": %.6f, "
            "\"device_s\": %.6f, \"apply_s\": %.6f, \"call_s\": %.6f, \"total_s\": %.6f, \"rank_docs\": %zu, \"host_threads\": %u, "
            "\"host_phases_s\": {\"batch\": %.6f, \"layout\": %.6f, \"pack_docs\": %.6f, \"distinct\": %.6f}, "
            "\"end_to_end_merges_per_s\": %.1f, \"pcie_inclusive_merges_per_s\": %.1f, "
-           "\"cpu_same_states_merges_per_s\": %.1f, \"sample_docs_checked\": %zu, \"sample_mismatches\": %zu}\n",
+           "\"cpu_same_states_merges_per_s\": %.1f, \"sample_docs_checked\": %zu, \"single_merge_docs_checked\": %zu, "
+           "\"sample_mismatches\": %zu}\n",
            n, E, (double)live / n, st.pack_s, st.device_s, st.apply_s, st.call_s, total, st.rank_docs, detail::host_threads(),
            st.batch_s, st.layout_s, st.docs_s, st.distinct_s,
-           merges / total, merges / st.device_s, merges / cpu_s, sample.size(), bad);
+           merges / total, merges / st.device_s, merges / cpu_s, n, sample.size(), bad);
     return bad ? 1 : 0;
 }

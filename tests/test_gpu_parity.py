@@ -909,11 +909,16 @@ def test_graph_replay_stress_worklist_paths(torch, kind):
 
 # ------------------------------------------------ host path: packed outputs, device order check
 
+@pytest.mark.parametrize("pinned", [False, True], ids=["copied", "pinned"])
 @pytest.mark.parametrize("what", ["join", "exchange", "fold_awset", "fold_delta"])
-def test_packed_batch_outputs(torch, what):
+def test_packed_batch_outputs(torch, what, pinned):
     """crdt_ctx_set_option("pack_batch_outputs", 1): the *_batch calls return
-    only live entries, doc d at the prefix sum of the counts; every document
-    bit-exact vs the oracle (large documents take the tile / block paths)."""
+    only live entries, doc d at the prefix sum of the counts (computed on the
+    device, pack_scan_kernel); every document bit-exact vs the oracle (large
+    documents take the tile / block paths).  pinned: the host outputs lie in
+    crdt_host_alloc blocks, so the gather kernel writes them itself (api.cpp
+    fetch_outputs) and the call's one sync is its last; copied: ordinary host
+    memory, gathered on the device and copied after one read-back of the totals."""
     rng = random.Random(hash(what) % 1000)
     R = 3
     e = crdtgpu.Engine(0)
@@ -922,15 +927,15 @@ def test_packed_batch_outputs(torch, what):
         if what in ("join", "exchange"):
             dst, src = join_case(rng, 1500, R, lambda: rng.choice([0, 1, 30, 64, 65, 300, 3000]), 10 ** 6, 40)
             if what == "join":
-                pairs = [(e.join(dst, src), oracle.join(dst, src))]
+                pairs = [(e.join(dst, src, pinned=pinned), oracle.join(dst, src))]
             else:
-                g1, g2 = e.exchange(dst, src)
+                g1, g2 = e.exchange(dst, src, pinned=pinned)
                 pairs = [(g1, oracle.join(dst, src)), (g2, oracle.join(src, dst))]
         else:
             mode = CRDT_FOLD_AWSET if what == "fold_awset" else CRDT_FOLD_DELTA
             dst, srcs = fold_case(rng, 1500, R, lambda: rng.randint(0, 80), lambda: rng.randint(0, 6),
                                   lambda: rng.randint(0, 12), lambda: rng.randint(0, 3), 300, 9, mode == CRDT_FOLD_DELTA)
-            pairs = [(e.fold(mode, dst, srcs), oracle.fold(mode, dst, srcs))]
+            pairs = [(e.fold(mode, dst, srcs, pinned=pinned), oracle.fold(mode, dst, srcs))]
         for got, (rc, want) in pairs:
             assert rc == 0
             n = dst.n_docs
@@ -940,6 +945,94 @@ def test_packed_batch_outputs(torch, what):
                 assert out_doc(got, d, R) == out_doc(want, d, R), d
     finally:
         e.close()
+
+
+@pytest.mark.parametrize("span", [1, 0], ids=["span", "per_array"])
+@pytest.mark.parametrize("shared", [False, True], ids=["own_keys", "shared_keys"])
+@pytest.mark.parametrize("pinned_out", [False, True], ids=["copied", "pinned"])
+def test_packed_exchange_counts_inputs(torch, span, shared, pinned_out):
+    """The host path's most staging-hungry call: crdt_awset_exchange_batch with
+    counts-bearing inputs (slack slots: 12 input arrays) in ordinary host
+    memory, packed outputs (two output rooms of six arrays, the packed offsets
+    and gathers), staged span-wise or array by array ("span_staging"): every
+    document of both directions exact, counts and offsets as packed."""
+    rng = random.Random(61)
+    R = 3
+    sz = lambda: rng.choice([0, 2, 40, 64, 65, 500, 2100])  # noqa: E731
+    dst = batch_of(R, [random_state(rng, R, sz(), 10 ** 6, 30) for _ in range(700)], slack=3)
+    src = batch_of(R, [random_state(rng, R, sz(), 10 ** 6, 30) for _ in range(700)], slack=1)
+    assert dst.counts is not None and src.counts is not None
+    e = crdtgpu.Engine(0)
+    try:
+        e.set_option("pack_batch_outputs", 1)
+        e.set_option("span_staging", span)
+        for _ in range(2):  # twice: the second call reuses every staging buffer
+            g1, g2 = e.exchange(dst, src, shared_keys=shared, pinned=pinned_out)
+        rc, w1 = oracle.join(dst, src)
+        assert rc == 0
+        rc, w2 = oracle.join(src, dst)
+        assert rc == 0
+        n = dst.n_docs
+        for got, want in ((g1, w1), (g2, w2)):
+            cnt = np.asarray(got.counts[:n]).astype(np.int64)
+            assert (cnt == np.asarray(want.counts[:n])).all()
+            assert (np.asarray(got.offsets[: n + 1]) == np.concatenate([[0], np.cumsum(cnt)])).all()
+            for d in range(n):
+                assert out_doc(got, d, R) == out_doc(want, d, R), d
+    finally:
+        e.close()
+
+
+@pytest.mark.parametrize("what", ["exchange_shared", "exchange", "join"])
+def test_padded_stores_stay_in_each_document(eng, torch, what):
+    """The wave kernel's padded whole-sector stores (join.hip,
+    CRDT_JOIN_PAD_STORES) write zeros into a document's slack slots past its
+    live entries (include/crdtgpu.h: slots past counts[d] are unspecified).
+    Outputs pre-filled with a sentinel: every document's live entries exact,
+    every slot a padded store wrote lies inside its own document's capacity
+    [dst.offsets[d] + src.offsets[d], dst.offsets[d+1] + src.offsets[d+1])
+    below 128 slots past its live count, and nothing past the batch's capacity
+    changed.  Inputs with slack (counts < slots) and without."""
+    rng = random.Random(63)
+    R = 2
+    sz = lambda: rng.choice([0, 1, 3, 7, 16, 33, 64])  # noqa: E731
+    docs_d = [random_state(rng, R, sz(), 400, 9) for _ in range(3000)]
+    docs_s = [random_state(rng, R, sz(), 400, 9) for _ in range(3000)]
+    dev = torch.device("cuda:0")
+    SENT = -0x5A5A5A5A5A5A5A5B
+    for slack in (0, 5):
+        a, b = batch_of(R, docs_d, slack=slack), batch_of(R, docs_s, slack=slack)
+        slots = int(a.offsets[-1]) + int(b.offsets[-1])
+        extra = 4096
+        outs = []
+        for k in range(2 if what.startswith("exchange") else 1):
+            o = OutBuffers(a.n_docs, R, slots + extra, device=dev,
+                           shared_keys=outs[0] if (k == 1 and what == "exchange_shared") else None)
+            for t in (o.keys, o.counters):
+                t.fill_(SENT)
+            o.actors.fill_(-0x5A5A5A5B)
+            outs.append(o)
+        if what == "join":
+            eng.join_async(a.to(dev), b.to(dev), outs[0])
+        else:
+            eng.exchange_async(a.to(dev), b.to(dev), outs[0], outs[1])
+        eng.sync()
+        wants = [oracle.join(a, b)[1]] + ([oracle.join(b, a)[1]] if len(outs) == 2 else [])
+        cap_lo = (np.asarray(a.offsets[:-1]).astype(np.int64) + np.asarray(b.offsets[:-1]))
+        cap_hi = (np.asarray(a.offsets[1:]).astype(np.int64) + np.asarray(b.offsets[1:]))
+        for o, want in zip(outs, wants):
+            h = host_out(o, torch)
+            assert_same(h, want, a.n_docs, R)
+            cnt = np.asarray(h.counts[: a.n_docs]).astype(np.int64)
+            for f, sent in (("keys", SENT & ((1 << 64) - 1)), ("counters", SENT & ((1 << 64) - 1)),
+                            ("actors", -0x5A5A5A5B & 0xFFFFFFFF)):
+                arr = np.asarray(getattr(h, f)).astype(np.uint64)
+                assert (arr[slots:] == sent).all(), (f, "written past the batch's capacity")
+                written = np.nonzero(arr[:slots] != sent)[0]
+                doc = np.searchsorted(cap_hi, written, side="right")  # the document whose capacity holds the slot
+                assert (written >= cap_lo[doc]).all()
+                rel = written - cap_lo[doc]
+                assert (rel < np.maximum(cnt[doc], 128)).all(), (f, "a padded store past 128 slots")
 
 
 def test_batch_key_order_checked_on_device(eng):
@@ -984,9 +1077,11 @@ def test_batch_key_order_checked_on_device(eng):
 @pytest.mark.parametrize("what", ["tile_join", "tile_exchange", "block_fold_awset", "block_fold_delta"])
 def test_unsorted_large_documents_never_reach_the_merge(eng, what):
     """An unsorted key in a tile-sized document (join / exchange: merge-path
-    tiles) or in a block-fold-sized document (> 256 tuples): the *_batch call
-    reads the device order check back before launching any merge kernel
-    (api.cpp order_gate) and returns CRDT_E_UNSORTED; the context stays usable."""
+    tiles) or in a block-fold-sized document (> 256 tuples): the device order
+    check closes the merge's gate, so the merge's first kernel returns at once
+    and nothing reaches the tile / block paths (Work::gate; no host read-back
+    before the launch); the *_batch call returns CRDT_E_UNSORTED and the
+    context stays usable."""
     rng = random.Random(77)
     R = 3
     if what.startswith("tile"):

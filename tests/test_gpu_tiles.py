@@ -5,9 +5,11 @@ documents of up to 2^20 entries per side).
 
 Bit-exact vs the C oracle (oracle/awset_oracle.c) on: tile boundaries that
 split a common key's (dst, src) pair, documents of 1 to 2^20 entries, the
-exchange (both directions from one read), the fallback to the per-document
-block kernel when the tiles exceed the workspace, and all 16,384 documents of
-BASELINE config 4 in both directions.
+exchange (both directions from one read), tile workspaces smaller than the
+call's tiles (passes of `join_tile_capacity` tiles, a document straddling
+them), the fallback to the per-document block kernel past the last pass, and
+all 16,384 documents of BASELINE config 4 in both directions, in one pass and
+in three.
 """
 
 import random
@@ -165,18 +167,30 @@ def test_tile_one_document_of_a_million(shaped):
     check_join_and_exchange(shaped, a, b, R)
 
 
+def host_tiles(a, b, tile=TILE // 2):
+    """Tiles a join of host batches a <- b has (tile.hip: ceil((nd + ns) / T) per
+    document with more than 64 live entries on a side; T = 1024 for the default
+    shape)."""
+    nd = np.array([a.live(d) for d in range(a.n_docs)], dtype=np.int64)
+    ns = np.array([b.live(d) for d in range(b.n_docs)], dtype=np.int64)
+    big = (nd > 64) | (ns > 64)
+    return int(((nd + ns + tile - 1) // tile)[big].sum())
+
+
 def test_tile_fallback_and_switch(eng):
-    """More tiles than the workspace holds -> the per-document block kernel;
-    join_tiles=0 -> block kernel always.  Same results either way."""
+    """More tiles than tile_max_passes x join_tile_capacity -> the per-document
+    block kernel; join_tiles=0 -> block kernel always.  Same results either way."""
     rng = random.Random(8)
     R = 2
     dsts = [random_state(rng, R, rng.choice([100, 5000, 9000]), 20000, 20) for _ in range(40)]
     srcs = [random_state(rng, R, rng.choice([100, 5000, 9000]), 20000, 20) for _ in range(40)]
     dst, src = batch_of(R, dsts), batch_of(R, srcs)
+    assert host_tiles(dst, src) > 3
     rc, want = oracle.join(dst, src)
     assert rc == 0
     try:
         eng.set_option("join_tile_capacity", 3)
+        eng.set_option("join_tile_max_passes", 1)
         assert_same(eng.join(dst, src), want, dst.n_docs, R)
         rc, want2 = oracle.join(src, dst)
         assert rc == 0
@@ -184,12 +198,77 @@ def test_tile_fallback_and_switch(eng):
         assert_same(o1, want, dst.n_docs, R)
         assert_same(o2, want2, dst.n_docs, R)
         eng.set_option("join_tile_capacity", 1 << 22)
+        eng.set_option("join_tile_max_passes", 256)
         eng.set_option("join_tiles", 0)
         assert_same(eng.join(dst, src), want, dst.n_docs, R)
     finally:
         eng.set_option("join_tiles", 1)
         eng.set_option("join_tile_capacity", 1 << 22)
+        eng.set_option("join_tile_max_passes", 256)
     assert_same(eng.join(dst, src), want, dst.n_docs, R)
+
+
+@pytest.mark.parametrize("cap", [1, 3, 7, 64])
+def test_tile_passes_small_capacity(eng, cap):
+    """A workspace of `cap` tiles: the tile path runs ceil(tiles / cap) passes
+    (tile.hip, launch_join_tiles), and a pass ends inside a document whenever
+    one straddles it -- cap 1 makes every tile its own pass, so every later
+    tile of a document takes its placed count from the carry word instead of a
+    look-back.  Join and exchange, host path (exact tile count), bit-exact."""
+    rng = random.Random(100 + cap)
+    R = 3
+    sz = lambda: rng.choice([0, 5, 64, 65, 1023, 1024, 2049, 7000])  # noqa: E731
+    dsts = [random_state(rng, R, sz(), 40000, 20) for _ in range(60)]
+    srcs = [random_state(rng, R, sz(), 40000, 20) for _ in range(60)]
+    dst, src = batch_of(R, dsts), batch_of(R, srcs)
+    tiles = host_tiles(dst, src)
+    assert tiles >= 2 * cap
+    try:
+        eng.set_option("join_tile_capacity", cap)
+        eng.set_option("join_tile_max_passes", 4096)
+        check_join_and_exchange(eng, dst, src, R)
+    finally:
+        eng.set_option("join_tile_capacity", 1 << 22)
+        eng.set_option("join_tile_max_passes", 256)
+
+
+def test_tile_passes_one_document_many_passes(eng, torch):
+    """One 2^17 + 2^17 document (256 tiles) in passes of 37 tiles, device-resident
+    through the async ABI (passes bounded from the batch size, most of them past
+    the call's tiles and returning at once): the carry crosses six pass
+    boundaries inside the document."""
+    rng = np.random.default_rng(12)
+    R = 2
+    n = 1 << 17
+    univ = np.sort(rng.choice(np.arange(3 * n, dtype=np.uint64), size=int(1.5 * n), replace=False))
+    pick = lambda: np.sort(rng.choice(univ, size=n, replace=False))  # noqa: E731
+
+    def side(keys):
+        return AWSetBatch(R, np.array([0, n], dtype=np.uint32), keys.astype(np.uint64),
+                          rng.integers(0, 2, n).astype(np.uint32), rng.integers(1, 1000, n).astype(np.uint64),
+                          rng.integers(0, 1000, R).astype(np.uint64))
+
+    a, b = side(pick()), side(pick())
+    rc, want = oracle.join(a, b)
+    assert rc == 0
+    rc, want2 = oracle.join(b, a)
+    assert rc == 0
+    dev = torch.device("cuda:0")
+    try:
+        eng.set_option("join_tile_capacity", 37)
+        eng.set_option("join_tile_max_passes", 65536)
+        eng.set_max_doc_entries(n)  # (the async bound then counts passes from the promise)
+        da, db = a.to(dev), b.to(dev)
+        o1 = OutBuffers(1, R, 2 * n, device=dev)
+        o2 = OutBuffers(1, R, 2 * n, device=dev)
+        eng.exchange_async(da, db, o1, o2)
+        eng.sync()
+    finally:
+        eng.set_option("join_tile_capacity", 1 << 22)
+        eng.set_option("join_tile_max_passes", 256)
+        eng.set_max_doc_entries()
+    assert_same(host_out(o1, torch), want, 1, R)
+    assert_same(host_out(o2, torch), want2, 1, R)
 
 
 @pytest.mark.parametrize("dispensers", [1, 8])
@@ -217,21 +296,29 @@ def _sub(h, d0, d1, R):
                       h.vv[d0 * R:d1 * R], None if h.counts is None else h.counts[d0:d1])
 
 
-def test_config4_full_size_exchange(eng, torch):
+@pytest.mark.parametrize("cap", [1 << 22, 300_000], ids=["one_pass", "three_passes"])
+def test_config4_full_size_exchange(eng, torch, cap):
     """BASELINE config 4 at its stated size: 16,384 docs, Zipf(1.1) sizes up to
     2^20, 50% concurrent add/remove conflicts, R = 2.  The exchange writes
     A<-B and B<-A; every document of both is compared with the oracle (in
-    chunks of documents, so the host copy stays bounded)."""
+    chunks of documents, so the host copy stays bounded).  Also with a tile
+    workspace of 300,000 tiles, below the call's 780,811: three passes."""
     n = 16384
     R = 2
     A, B, total = gen_zipf(eng, torch, n)
     dev = torch.device("cuda:0")
     oab = OutBuffers(n, R, 2 * total, device=dev)
     oba = OutBuffers(n, R, 2 * total, device=dev)
-    eng.exchange_async(A.as_batch(), B.as_batch(), oab, oba)
-    eng.sync()
+    try:
+        eng.set_option("join_tile_capacity", cap)
+        eng.exchange_async(A.as_batch(), B.as_batch(), oab, oba)
+        eng.sync()
+    finally:
+        eng.set_option("join_tile_capacity", 1 << 22)
     ha, hb = host_out(A, torch).as_batch(), host_out(B, torch).as_batch()
     del A, B
+    if cap < (1 << 22):
+        assert host_tiles(ha, hb) > 2 * cap  # at least three passes
     for o, (x, y) in ((oab, (ha, hb)), (oba, (hb, ha))):
         ho = host_out(o, torch)
         oo = np.asarray(ho.offsets).astype(np.int64)

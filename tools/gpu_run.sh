@@ -25,6 +25,8 @@
 #   ptest    pytest -m gpu on $PTEST (a -k expression)
 #   jab      config-2 exchange timed per library build ($JLIBS: base = the product library, X = tools/libcrdtgpu_X.so)
 #   ftime    fold timing builds tools/fold_time_$FTIME (space-separated variant names), interleaved, configs 3 and 5
+#   tpass    config-4 exchange in passes of $TCAPS tiles vs one pass (tools/tile_passes.py)
+#   bench1   boundary_bench alone (C++ mirror ExchangeBatch, every document checked)
 set -u
 cd "$(dirname "$0")/.."
 source tools/gpu_step.sh
@@ -134,6 +136,11 @@ for r in "$@"; do
       done ;;
     xab)
       TAILN=12 step xab_$TAG 400 python3 tools/exchange_ab.py ;;
+    tpass)
+      TAILN=14 step tpass_$TAG 300 python3 tools/tile_passes.py 16384 ${TCAPS:-4194304 400000 300000} ;;
+    bench1)
+      TAILN=2 step boundary_$TAG 300 go-crdt-playground_amd/host/build/boundary_bench 65536
+      TAILN=12 step boundary_stages_$TAG 300 env CRDT_TRACE_STAGE=1 go-crdt-playground_amd/host/build/boundary_bench 65536 ;;
     ptest)
       TAILN=6 step ptest_$TAG 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -k "$PTEST"
       if grep -q " FAILED\| ERROR" gpurun_out/ptest_$TAG.log; then echo "tests failed"; exit 1; fi ;;
