@@ -106,6 +106,12 @@ namespace crdt {
 #ifndef CRDT_FOLD_DIAG_NOLOAD
 #define CRDT_FOLD_DIAG_NOLOAD 0
 #endif
+#ifndef CRDT_FOLD_DIAG_SKIP_CLASSIFY  // diagnostic: no classify pass (keys read, nothing kept but the document)
+#define CRDT_FOLD_DIAG_SKIP_CLASSIFY 0
+#endif
+#ifndef CRDT_FOLD_DIAG_SKIP_WALK  // diagnostic: no slot walk (nothing written)
+#define CRDT_FOLD_DIAG_SKIP_WALK 0
+#endif
 // CRDT_FOLD_PAD_STORES (with CRDT_FOLD_STAGE_STORES 1, diagnostic): each array's
 // staged stores run on to the end of the last survivor's cache line, within
 // the document's output capacity (slack past the live count is unspecified),
@@ -145,6 +151,11 @@ namespace crdt {
 // the source's entries only on a possible hit (see the classify pass).
 #ifndef CRDT_FOLD_TOMB_TAB
 #define CRDT_FOLD_TOMB_TAB 1
+#endif
+// CRDT_FOLD_FUSED: the lean delta pass's documents with no full step classified
+// and walked in one pass (fused_delta_walk)
+#ifndef CRDT_FOLD_FUSED
+#define CRDT_FOLD_FUSED 1
 #endif
 // pointer to global (address space 1) memory
 template <typename T>
@@ -755,6 +766,169 @@ __device__ __forceinline__ bool dense_delta_walk(Smem& m, const uint64_t (&key)[
     return true;
 }
 
+// The lean delta pass's common case in one pass over the tuples: no step is a
+// full merge (every Counter(src.Actor) > 0, awset-delta_test.go:53), at most
+// 15 sources, every key of the document within 256 ids and no actor == len(VV).
+// The classify (MakeDeltaMergeData, awset-delta_test.go:79-105: changed
+// entries, tombstones not re-added in their source) and the slot walk's add /
+// drop times (dense_delta_walk, no-full form) are computed from the same
+// registers, so the tuples and clocks are read from LDS once:
+//   1. every tuple's key, actor and counter into registers; the span and actor
+//      checks (a document that fails one is left to the two-pass form, LDS
+//      untouched: returns 0);
+//   2. the re-add check: a table of the steps with an entry per key slot
+//      (est, in svv -- dead without a full step), then each tombstone looks its
+//      slot up, searching its source's entries only when the bit is set (an
+//      entry of that key in the source, whose dot decides);
+//   3. the slot words (tk and svv, dead now): document entries add at time 0,
+//      changed entries (!HasDot(V_j, dot)) add at 2j+1, effective tombstones
+//      whose dot V_j lacks drop at 2j+2 (awset-delta_test.go:126-164); the
+//      slot's last entry is an atomic max of (time << 8 | tuple);
+//   4. a step with neither a changed entry nor an effective tombstone is a no-op
+//      (:60), under which the prefix-max clocks are not the exact ones: the
+//      document is left to the general kernel (returns 2);
+//   5. each slot resolves as in dense_delta_walk (returns 1).
+// Exactly the rule of the two-pass form (same times, same words).
+template <class Smem>
+__device__ __forceinline__ int fused_delta_walk(Smem& m, const uint32_t (&step)[4], const bool (&isE)[4],
+                                                const bool (&isT)[4], uint32_t N, uint32_t n, uint32_t ms, uint32_t R,
+                                                uint32_t cmax, uint32_t lane, Emit<4>& e, uint32_t& U) {
+    static_assert(sizeof(m.tk) >= 2 * 256 * 4 && sizeof(m.svv) >= 256 * 4, "fused_delta_walk: slot words");
+    if (N == 0 || ms > 15) return 0;
+    // (registers: only the slots stay live across the passes; actors and
+    // counters are re-read from ta / tc, which no pass below overwrites)
+    uint32_t sl[4];
+    uint64_t b;
+    {
+        uint64_t key[4];
+        bool bad = false;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const uint32_t i = c * 64u + lane, ii = i < N ? i : N - 1u;  // (lanes past N: copies of the last tuple)
+            const bool in = (uint32_t)c * 64u < N;
+            key[c] = in ? m.tk[ii] : 0ull;
+            bad |= in && m.ta[ii] == R;
+        }
+        b = readlane64(key[0], 0);
+        uint32_t lo = ~0u, hi = 0u;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            if ((uint32_t)c * 64u >= N) continue;
+            const uint64_t d = key[c] - b + 0x80000000ull;
+            bad |= (d >> 32) != 0;
+            lo = min(lo, (uint32_t)d);
+            hi = max(hi, (uint32_t)d);
+        }
+        if (ballot(bad)) return 0;
+        lo = wave_minmax<false>(lo);
+        hi = wave_minmax<true>(hi);
+        if (hi - lo >= 256u) return 0;
+        b = b - 0x80000000ull + lo;  // key of slot 0
+#pragma unroll
+        for (int c = 0; c < 4; ++c) sl[c] = (uint32_t)(key[c] - b) & 255u;
+    }
+    const uint64_t kb = b;
+    // 2. re-add check
+    uint32_t* est = reinterpret_cast<uint32_t*>(m.svv);
+    reinterpret_cast<uint4*>(est)[lane] = make_uint4(0u, 0u, 0u, 0u);
+    wave_sync();
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+        if ((uint32_t)c * 64u < N && isE[c]) atomicOr(&est[sl[c]], 1u << (step[c] & 63u));
+    wave_sync();
+    uint32_t eff = 0;  // bit c: the lane's tuple of chunk c is an effective tombstone
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        if ((uint32_t)c * 64u >= N || !isT[c]) continue;
+        const uint32_t j = step[c] & 63u;
+        bool f = true;
+        if ((est[sl[c]] >> j) & 1u) {  // an entry of this slot in source j: is it this key, re-added?
+            const uint32_t i = c * 64u + lane;
+            const uint64_t k = m.tk[i];
+            const uint32_t s0 = m.soff[j], lo2 = n + s0, len = m.soff[j + 1] - s0;
+            uint32_t pos = 0;
+            for (uint32_t st = 256; st > 0; st >>= 1) {
+                if (st > cmax) continue;
+                const bool in = pos + st <= len;
+                const uint64_t v2 = m.tk[in ? lo2 + pos + st - 1 : 0u];
+                pos += (in && v2 < k) ? st : 0u;
+            }
+            const bool in_s = pos < len && m.tk[lo2 + pos] == k;
+            f = !(in_s && (m.ta[lo2 + pos] != m.ta[i] || m.tc[lo2 + pos] > m.tc[i]));
+        }
+        eff |= f ? (1u << c) : 0u;
+    }
+    // 3. slot words (every read of tk and est is issued above: LDS runs a wave's operations in order)
+    uint32_t* erows = reinterpret_cast<uint32_t*>(m.tk);  // [256] last entry: time << 8 | tuple
+    uint32_t* addw = erows + 256;                          // [256] add times
+    uint32_t* dropw = est;                                 // [256] drop times
+    const uint4 z4 = make_uint4(0u, 0u, 0u, 0u);
+    reinterpret_cast<uint4*>(erows)[lane] = z4;
+    reinterpret_cast<uint4*>(addw)[lane] = z4;
+    reinterpret_cast<uint4*>(dropw)[lane] = z4;
+    wave_sync();
+    uint64_t me = 0, mt = 0;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        const uint32_t i = c * 64u + lane;
+        if ((uint32_t)c * 64u >= N) continue;
+        const uint32_t ii = i < N ? i : 0u;
+        const uint32_t a = m.ta[ii];
+        const uint64_t cc = m.tc[ii];
+        if (i >= N) continue;
+        const uint32_t j = step[c] & 63u;
+        const bool cov = a < R;  // (actor > R: HasDot false; == R was excluded)
+        const bool seen = cov && m.vs[j * R + (cov ? a : 0u)] >= cc;  // HasDot(V_j, dot)
+        if (i < n) {
+            atomicOr(&addw[sl[c]], 1u);
+            atomicMax(&erows[sl[c]], i);
+        } else if (isE[c]) {
+            if (!seen) {
+                const uint32_t r = 2u * j + 1u;
+                me |= 1ull << j;
+                atomicOr(&addw[sl[c]], 1u << r);
+                atomicMax(&erows[sl[c]], (r << 8) | i);
+            }
+        } else if ((eff >> c) & 1u) {
+            mt |= 1ull << j;
+            if (!seen) atomicOr(&dropw[sl[c]], 1u << (2u * j + 2u));
+        }
+    }
+    // 4. a no-op step: the general kernel replays the steps one by one
+    if (low_mask(ms) & ~wave_or64(me) & ~wave_or64(mt)) return 2;
+    wave_sync();
+    // 5. resolve each slot
+    uint32_t aw[4], dw[4], lt8[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const uint32_t s = q * 64u + lane;
+        aw[q] = addw[s];
+        dw[q] = dropw[s];
+        lt8[q] = erows[s] & 0xFFu;
+    }
+    uint32_t ea[4];
+    uint64_t ec[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        ea[q] = m.ta[lt8[q]];
+        ec[q] = m.tc[lt8[q]];
+    }
+    uint32_t base = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const uint32_t s = q * 64u + lane;
+        const bool P = aw[q] != 0u && (dw[q] >> (31u - (uint32_t)__clz(aw[q]))) == 0u;
+        const uint64_t pm = ballot(P);
+        e.k[q] = kb + s;
+        e.a[q] = P ? ea[q] : 0u;
+        e.c[q] = P ? ec[q] : 0ull;
+        e.off[q] = P ? base + below(pm) : kOOB;
+        base += popc(pm);
+    }
+    U = base;
+    return 1;
+}
+
 template <int EPL, bool DELTA, int NQ, class Smem>
 __device__ __forceinline__ uint32_t sort_resolve(Smem& m, uint32_t Kc, uint32_t ms, uint32_t R,
                                                  uint64_t full_mask, uint32_t lane, uint64_t lt, Emit<NQ>& e,
@@ -1360,6 +1534,24 @@ __global__ __launch_bounds__(fold_waves<DELTA>() * 64) __attribute__((amdgpu_wav
                 cmax = (uint32_t)__builtin_amdgcn_readlane((int)cmax, 63);  // ... whose last lane has the maximum
             }
             STAMP(11)
+            // CRDT_FOLD_FUSED: the lean delta pass's common case, classify and slot
+            // walk in one pass (fused_delta_walk); 0: the two-pass form below
+            // The lean delta pass then holds nothing else: a document the fused pass
+            // does not take (a full step, a no-op step, > 15 sources, a key span of
+            // 256 or more, an actor == len(VV)) is left to the general kernel.
+            constexpr bool kFused = DELTA && LEAN && NCH == 4 && CRDT_FOLD_FUSED;
+            if constexpr (kFused) {
+                const int fused =
+                    full_mask == 0ull ? fused_delta_walk(m, step, isE, isT, N, n, ms, R, cmax, lane, em, U) : 0;
+                if (fused != 1) {  // left to the general kernel, nothing written here
+                    deferred = true;
+                    if (lane == 0) push_defer(wk, cur.d, n_docs);
+#pragma unroll
+                    for (int q = 0; q < NCH; ++q) em.off[q] = kOOB;
+                    U = 0;
+                }
+            }
+            if constexpr (!kFused) {
             // CRDT_FOLD_TOMB_TAB: est[key & 255] = the steps (< 32) with an entry of that
             // low key byte, so a tombstone whose step bit is clear was not re-added in
             // its source (effective) without the binary search below; a set bit (the
@@ -1379,6 +1571,10 @@ __global__ __launch_bounds__(fold_waves<DELTA>() * 64) __attribute__((amdgpu_wav
 #pragma unroll
             for (int c = 0; c < NCH; ++c) {
                 key[c] = 0;
+                if (CRDT_FOLD_DIAG_SKIP_CLASSIFY && (uint32_t)c < NQ) {  // diagnostic: keys only
+                    key[c] = m.tk[c * 64u + lane < N ? c * 64u + lane : 0u];
+                    continue;
+                }
                 if ((uint32_t)c < NQ) {
                     const uint32_t i = c * 64u + lane;
                     const uint32_t ii = i < N ? i : 0u;
@@ -1461,6 +1657,7 @@ __global__ __launch_bounds__(fold_waves<DELTA>() * 64) __attribute__((amdgpu_wav
                 const uint64_t anye = wave_or64(me);
                 tmask = wave_or64(mt) & low_mask(ms);
                 noop_mask = low_mask(ms) & ~full_mask & ~anye & ~tmask;
+                if (CRDT_FOLD_DIAG_SKIP_CLASSIFY) noop_mask = 0;  // (diagnostic: no replay either)
             }
             if (DELTA && noop_mask) {
                 // a step brings nothing: replay the schedule step by step with the exact clocks
@@ -1514,9 +1711,17 @@ __global__ __launch_bounds__(fold_waves<DELTA>() * 64) __attribute__((amdgpu_wav
             bool walked = false;
             if constexpr (!DELTA)
                 walked = dense_awset_walk<NCH>(m, key, step, N, n, ms, R, lane, lt, em, U, err);
-            else if constexpr (NCH == 4)
-                walked = dense_delta_walk(m, key, step, isE, isT, flag, full_mask, noop_mask, N, n, ms, R, lane, lt,
-                                          em, U STAMP_ARGS);
+            else if constexpr (NCH == 4) {
+                if (CRDT_FOLD_DIAG_SKIP_WALK) {  // diagnostic: nothing resolved, nothing written
+                    walked = true;
+                    U = 0;
+#pragma unroll
+                    for (int q = 0; q < NCH; ++q) em.off[q] = kOOB, em.k[q] = key[q], em.a[q] = flag, em.c[q] = 0;
+                } else {
+                    walked = dense_delta_walk(m, key, step, isE, isT, flag, full_mask, noop_mask, N, n, ms, R, lane,
+                                              lt, em, U STAMP_ARGS);
+                }
+            }
             if (LEAN && !walked) {  // left to the general kernel: nothing written here
                 deferred = true;
                 if (lane == 0) push_defer(wk, cur.d, n_docs);
@@ -1557,6 +1762,7 @@ __global__ __launch_bounds__(fold_waves<DELTA>() * 64) __attribute__((amdgpu_wav
                 U = Kc <= 64 ? sort_resolve<1, DELTA>(m, Kc, ms, R, full_mask, lane, lt, em, err STAMP_ARGS)
                              : sort_resolve<2, DELTA>(m, Kc, ms, R, full_mask, lane, lt, em, err STAMP_ARGS);
             }
+            }  // !kFused
             STAMP(5)
         }
         // ---- write the survivors (every store unconditional)
