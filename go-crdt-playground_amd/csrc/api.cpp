@@ -8,6 +8,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <initializer_list>
 #include <map>
 #include <mutex>
 #include <new>
@@ -25,12 +26,16 @@ hipError_t launch_fold(int mode, const BatchView& dst, const SrcView& sb, const 
                        const Work& wk, uint32_t block_grid, bool lean_first, hipStream_t stream);
 uint32_t tile_positions(uint32_t shape);
 hipError_t sort_storage(uint32_t n_docs, uint32_t n_slots, size_t* bytes);
-hipError_t launch_check_order(const uint32_t* off, const uint32_t* cnt, uint32_t n, const uint64_t* keys,
-                              uint32_t* status, uint32_t n_cu, hipStream_t stream);
-hipError_t launch_pack_scan(const uint32_t* off, const uint32_t* cnt, uint32_t n, uint32_t* poff, uint32_t* host_off,
-                            const uint32_t* gate, hipStream_t stream);
-hipError_t launch_pack_out(const OutView& in, const uint32_t* poff, uint32_t n, uint32_t R, const OutView& out,
-                           const uint32_t* gate, uint32_t n_cu, hipStream_t stream);
+struct OrderRanges {  // pack.hip: one list of key ranges whose order is checked
+    const uint32_t* off;
+    const uint32_t* cnt;
+    uint32_t n;
+    const uint64_t* keys;
+};
+hipError_t launch_check_order(const void* sets, uint32_t n_sets, uint32_t* status, uint32_t n_cu, hipStream_t stream);
+hipError_t launch_pack(uint32_t nout, const OutView* in, uint32_t* const* poff, uint32_t* const* host_off,
+                       const OutView* out, uint32_t n, uint32_t R, const uint32_t* gate, uint32_t* host_status,
+                       uint32_t n_cu, hipStream_t stream);
 hipError_t launch_sort(const BatchView& in, uint32_t n_slots, const OutView& out, void* temp, size_t temp_bytes,
                        uint32_t* ends, uint32_t* idx, uint32_t* status, uint32_t n_cu, hipStream_t stream);
 hipError_t launch_apply(const BatchView& st, const TombView& tb, const ApplyOps& ops, const OutView& out,
@@ -192,6 +197,12 @@ struct crdt_ctx {
     // set by a *_batch call around its merge launch: the merge's first kernel is
     // gated on the status word its order checks wrote (Work::gate)
     bool call_gate = false;
+    // set by a *_batch call whose host arrays show no document above 64 live
+    // entries on a side: the join launches no large-document path at all
+    bool call_small = false;
+    // page-locked word the packed-output gather copies the status word into, so
+    // a host-path call reads its verdict without another runtime call
+    uint32_t* host_status = nullptr;
     hipStream_t stream = nullptr;
     // Ordering of the shared workspace across streams: the last call's stream
     // and an event recorded after its launches.  A call on another stream
@@ -350,6 +361,8 @@ int crdt_ctx_create(int device, crdt_ctx** out) {
     if (rc == CRDT_OK) rc = ctx->parts.reserve((size_t)kCtxParts * CRDT_MAX_R * sizeof(uint64_t));
     if (rc == CRDT_OK) rc = hip_err(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
     if (rc == CRDT_OK) rc = hip_err(hipEventCreateWithFlags(&ctx->last_ev, hipEventDisableTiming));
+    if (rc == CRDT_OK && hipHostMalloc(reinterpret_cast<void**>(&ctx->host_status), 64, hipHostMallocDefault) != hipSuccess)
+        ctx->host_status = nullptr;  // (then the host path reads the status word back instead)
     if (rc != CRDT_OK) {
         crdt_ctx_destroy(ctx);
         return rc;
@@ -370,6 +383,7 @@ void crdt_ctx_destroy(crdt_ctx* ctx) {
     if (ctx->last_ev) (void)hipEventDestroy(ctx->last_ev);
     for (void* p : ctx->retired) (void)hipFree(p);
     ctx->retired.clear();
+    if (ctx->host_status) (void)hipHostFree(ctx->host_status);
     ctx->ws.release();
     ctx->worklist.release();
     ctx->defer.release();
@@ -511,7 +525,7 @@ static int join_common(crdt_ctx* ctx, const crdt_awset_batch* dst, const crdt_aw
     rc = enter(ctx, s, cap);
     if (rc == CRDT_OK) rc = grow(ctx->worklist, std::max<size_t>(dst->n_docs, 1) * sizeof(uint32_t), cap);
     if (rc != CRDT_OK) return rc;
-    const bool no_large = ctx->max_doc_entries <= 64;
+    const bool no_large = ctx->max_doc_entries <= 64 || ctx->call_small;
     TileWork tw{};
     const bool tiles = !no_large && ctx->join_tiles;
     if (tiles) {
@@ -1075,8 +1089,9 @@ int fetch_out(const crdt_awset_out* h, const crdt_awset_out& d, uint32_t n_docs,
 // The key order of a staged batch (ranges off[r] .. + counts or off[r + 1]),
 // checked on the device; a violation sets kErrUnsorted in the status word, which
 // closes the merge's gate (Work::gate) and reads back as CRDT_E_UNSORTED.
-int check_order(crdt_ctx* ctx, const uint32_t* off, const uint32_t* cnt, uint32_t n, const uint64_t* keys) {
-    return hip_err(launch_check_order(off, cnt, n, keys, ctx->ws.as<uint32_t>(64), (uint32_t)ctx->n_cu, ctx->stream));
+int check_order(crdt_ctx* ctx, std::initializer_list<OrderRanges> sets) {
+    return hip_err(launch_check_order(sets.begin(), (uint32_t)sets.size(), ctx->ws.as<uint32_t>(64),
+                                      (uint32_t)ctx->n_cu, ctx->stream));
 }
 
 // The merge launch of a host-path call, gated on the device by its order checks.
@@ -1086,6 +1101,7 @@ int gated(crdt_ctx* ctx, F&& launch) {
     const int rc = launch();
     ctx->call_gate = false;
     ctx->call_tiles = 0;
+    ctx->call_small = false;
     return rc;
 }
 
@@ -1093,7 +1109,6 @@ int gated(crdt_ctx* ctx, F&& launch) {
 // per document with more than 64 live entries on a side), so the tile path
 // launches exactly the passes it needs (join_common).
 uint64_t host_tiles(const crdt_ctx* ctx, const crdt_awset_batch* a, const crdt_awset_batch* b) {
-    if (ctx->max_doc_entries <= 64 || !ctx->join_tiles) return 0;
     const uint64_t T = tile_positions(ctx->tile_shape);
     uint64_t t = 0;
     for (uint32_t d = 0; d < a->n_docs; ++d) {
@@ -1101,7 +1116,25 @@ uint64_t host_tiles(const crdt_ctx* ctx, const crdt_awset_batch* a, const crdt_a
         const uint64_t ns = b->counts ? b->counts[d] : b->offsets[d + 1] - b->offsets[d];
         if (nd > 64 || ns > 64) t += (nd + ns + T - 1) / T;
     }
-    return std::max<uint64_t>(t, 1);
+    return t;
+}
+
+// Before a host-path join's launch: the exact tile count, or no large-document
+// path at all when no document has one (six launches fewer; 0 tiles <=> no
+// document above 64 live entries on a side, whatever the tile options).
+void plan_tiles(crdt_ctx* ctx, const crdt_awset_batch* a, const crdt_awset_batch* b) {
+    const uint64_t t = host_tiles(ctx, a, b);
+    ctx->call_small = t == 0;
+    ctx->call_tiles = std::max<uint64_t>(t, 1);
+}
+
+// The end of a host-path call: its one sync, then its status (read from the
+// page-locked copy the gather kernel made when `copied`, else read back).
+int finish(crdt_ctx* ctx, bool copied) {
+    if (!copied || !ctx->host_status) return crdt_ctx_sync(ctx, ctx->stream);
+    if (hipStreamSynchronize(ctx->stream) != hipSuccess) return CRDT_E_HIP;
+    const uint32_t st = __atomic_load_n(ctx->host_status, __ATOMIC_ACQUIRE);
+    return st ? crdt_ctx_sync(ctx, ctx->stream) : CRDT_OK;  // (an error: the usual read-back and reset)
 }
 
 // Download merge outputs.  Default: at their capacity offsets, as the kernels
@@ -1113,7 +1146,8 @@ uint64_t host_tiles(const crdt_ctx* ctx, const crdt_awset_batch* a, const crdt_a
 // outputs come back in ONE read-back before their copies.  keys[i] = false: an
 // exchange's second output sharing the first's key column.
 int fetch_outputs(crdt_ctx* ctx, Stager& st, int nout, const crdt_awset_out* const* h, const crdt_awset_out* d,
-                  const bool* keys, uint32_t n, uint32_t R, size_t slots) {
+                  const bool* keys, uint32_t n, uint32_t R, size_t slots, bool* status_copied) {
+    *status_copied = false;
     if (!ctx->pack_outputs) {
         int rc = CRDT_OK;
         for (int i = 0; i < nout && rc == CRDT_OK; ++i) rc = fetch_out(h[i], d[i], n, R, slots, ctx->stream, keys[i]);
@@ -1143,13 +1177,10 @@ int fetch_outputs(crdt_ctx* ctx, Stager& st, int nout, const crdt_awset_out* con
         }
     }
     if (st.rc != CRDT_OK) return st.rc;
-    int rc = CRDT_OK;
-    for (int i = 0; i < nout && rc == CRDT_OK; ++i) {
-        const uint32_t* gate = ctx->ws.as<uint32_t>(64);
-        rc = hip_err(launch_pack_scan(d[i].offsets, d[i].counts, n, poff[i], hoff[i], gate, ctx->stream));
-        if (rc == CRDT_OK)
-            rc = hip_err(launch_pack_out(view(&d[i]), poff[i], n, R, pk[i], gate, (uint32_t)ctx->n_cu, ctx->stream));
-    }
+    const OutView in[2] = {view(&d[0]), nout > 1 ? view(&d[1]) : OutView{}};
+    int rc = hip_err(launch_pack((uint32_t)nout, in, poff, hoff, pk, n, R, ctx->ws.as<uint32_t>(64), ctx->host_status,
+                                 (uint32_t)ctx->n_cu, ctx->stream));
+    *status_copied = rc == CRDT_OK && ctx->host_status != nullptr;
     if (rc != CRDT_OK || (zc[0] && (nout < 2 || zc[1]))) return rc;
     uint32_t tot[2] = {0, 0};
     for (int i = 0; i < nout && rc == CRDT_OK; ++i)
@@ -1272,15 +1303,16 @@ int crdt_awset_join_batch(crdt_ctx* ctx, const crdt_awset_batch* dst, const crdt
     crdt_awset_out dout = stage_out(st, dst->n_docs, dst->R, slots);
     st.flush();  // the inputs' span, if they lie in one crdt_host_alloc block
     if (st.rc != CRDT_OK) return st.rc;
-    rc = check_order(ctx, dd.offsets, dd.counts, dd.n_docs, dd.keys);
-    if (rc == CRDT_OK) rc = check_order(ctx, ds.offsets, ds.counts, ds.n_docs, ds.keys);
-    ctx->call_tiles = host_tiles(ctx, dst, src);
+    rc = check_order(ctx, {{dd.offsets, dd.counts, dd.n_docs, dd.keys}, {ds.offsets, ds.counts, ds.n_docs, ds.keys}});
+    plan_tiles(ctx, dst, src);
     if (rc == CRDT_OK) rc = gated(ctx, [&] { return crdt_awset_join_async(ctx, &dd, &ds, &dout, ctx->stream); });
     const crdt_awset_out* hs[1] = {out};
     const bool keys[1] = {true};
-    if (rc == CRDT_OK) rc = fetch_outputs(ctx, st, 1, hs, &dout, keys, dst->n_docs, dst->R, slots);
+    bool copied = false;
+    if (rc == CRDT_OK) rc = fetch_outputs(ctx, st, 1, hs, &dout, keys, dst->n_docs, dst->R, slots, &copied);
     ctx->call_tiles = 0;
-    const int sync = crdt_ctx_sync(ctx, ctx->stream);
+    ctx->call_small = false;
+    const int sync = finish(ctx, copied);
     return rc != CRDT_OK ? rc : sync;
 }
 
@@ -1308,17 +1340,18 @@ int crdt_awset_exchange_batch(crdt_ctx* ctx, const crdt_awset_batch* a, const cr
     const bool share = out_ab->keys == out_ba->keys;
     if (share) o[1].keys = o[0].keys;
     pc.mark("stage issued");
-    rc = check_order(ctx, da.offsets, da.counts, da.n_docs, da.keys);
-    if (rc == CRDT_OK) rc = check_order(ctx, db.offsets, db.counts, db.n_docs, db.keys);
-    ctx->call_tiles = host_tiles(ctx, a, b);
+    rc = check_order(ctx, {{da.offsets, da.counts, da.n_docs, da.keys}, {db.offsets, db.counts, db.n_docs, db.keys}});
+    plan_tiles(ctx, a, b);
     if (rc == CRDT_OK) rc = gated(ctx, [&] { return crdt_awset_exchange_async(ctx, &da, &db, &o[0], &o[1], ctx->stream); });
     pc.mark("order checks + kernels issued");
     const crdt_awset_out* hs[2] = {out_ab, out_ba};
     const bool keys[2] = {true, !share};
-    if (rc == CRDT_OK) rc = fetch_outputs(ctx, st, 2, hs, o, keys, a->n_docs, a->R, slots);
+    bool copied = false;
+    if (rc == CRDT_OK) rc = fetch_outputs(ctx, st, 2, hs, o, keys, a->n_docs, a->R, slots, &copied);
     ctx->call_tiles = 0;
+    ctx->call_small = false;
     pc.mark("fetches issued");
-    const int sync = crdt_ctx_sync(ctx, ctx->stream);
+    const int sync = finish(ctx, copied);
     pc.mark("synced");
     return rc != CRDT_OK ? rc : sync;
 }
@@ -1359,14 +1392,15 @@ int crdt_awset_fold_batch(crdt_ctx* ctx, int mode, const crdt_awset_batch* dst, 
     crdt_awset_out dout = stage_out(st, dst->n_docs, dst->R, total);
     st.flush();  // the inputs' span, if they lie in one crdt_host_alloc block
     if (st.rc != CRDT_OK) return st.rc;
-    rc = check_order(ctx, dd.offsets, dd.counts, dd.n_docs, dd.keys);
-    if (rc == CRDT_OK) rc = check_order(ctx, ds.entry_off, nullptr, ns, ds.keys);
-    if (rc == CRDT_OK && srcs->tomb_off) rc = check_order(ctx, ds.tomb_off, nullptr, ns, ds.tkeys);
+    rc = srcs->tomb_off ? check_order(ctx, {{dd.offsets, dd.counts, dd.n_docs, dd.keys}, {ds.entry_off, nullptr, ns, ds.keys},
+                                            {ds.tomb_off, nullptr, ns, ds.tkeys}})
+                        : check_order(ctx, {{dd.offsets, dd.counts, dd.n_docs, dd.keys}, {ds.entry_off, nullptr, ns, ds.keys}});
     if (rc == CRDT_OK) rc = gated(ctx, [&] { return crdt_awset_fold_async(ctx, mode, &dd, &ds, &dout, ctx->stream); });
     const crdt_awset_out* hs[1] = {out};
     const bool keys[1] = {true};
-    if (rc == CRDT_OK) rc = fetch_outputs(ctx, st, 1, hs, &dout, keys, dst->n_docs, dst->R, total);
-    const int sync = crdt_ctx_sync(ctx, ctx->stream);
+    bool copied = false;
+    if (rc == CRDT_OK) rc = fetch_outputs(ctx, st, 1, hs, &dout, keys, dst->n_docs, dst->R, total, &copied);
+    const int sync = finish(ctx, copied);
     return rc != CRDT_OK ? rc : sync;
 }
 

@@ -36,7 +36,11 @@
 
 #include <algorithm>
 #include <chrono>
+#include <condition_variable>
+#include <functional>
+#include <mutex>
 #include <cstdint>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <map>
@@ -301,6 +305,78 @@ inline unsigned host_threads() {
     return n;
 }
 
+// The worker threads, started once and kept: a thread started and ended per
+// phase allocates through a fresh malloc arena and returns its memory when it
+// ends, and on the GPU box that address-space churn (heap growth and release
+// in the C library's per-thread arenas) made every HIP runtime call of the
+// next device phase block ~1.3 ms (profiles/r06n_boundary_malloc_arenas.log:
+// with at most 4 arenas the device phase of the same call took 6 ms instead of
+// 25).  Kept threads keep their arenas and their scratch (thread_local below),
+// so a steady stream of batch calls allocates almost nothing on the host.
+class WorkerPool {
+   public:
+    explicit WorkerPool(unsigned n) {
+        for (unsigned i = 0; i < n; ++i) th_.emplace_back([this, i] { loop(i); });
+    }
+    ~WorkerPool() {
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        for (auto& t : th_) t.join();
+    }
+    unsigned size() const { return (unsigned)th_.size(); }
+    // run(i) for i in [0, jobs) -- job 0 on the calling thread, job i on worker i - 1
+    // (callers on several threads take turns; jobs <= size() + 1)
+    void run(unsigned jobs, const std::function<void(unsigned)>& f) {
+        std::lock_guard<std::mutex> turn(run_mu_);
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            job_ = &f;
+            jobs_ = jobs;
+            left_ = jobs - 1;
+            ++round_;
+        }
+        cv_.notify_all();
+        f(0);
+        std::unique_lock<std::mutex> lk(mu_);
+        done_.wait(lk, [this] { return left_ == 0; });
+        job_ = nullptr;
+    }
+
+   private:
+    void loop(unsigned i) {
+        uint64_t seen = 0;
+        for (;;) {
+            const std::function<void(unsigned)>* f = nullptr;
+            {
+                std::unique_lock<std::mutex> lk(mu_);
+                cv_.wait(lk, [&] { return stop_ || round_ != seen; });
+                if (stop_) return;
+                seen = round_;
+                if (i + 1 >= jobs_) continue;
+                f = job_;
+            }
+            (*f)(i + 1);
+            std::lock_guard<std::mutex> lk(mu_);
+            if (--left_ == 0) done_.notify_one();
+        }
+    }
+    std::vector<std::thread> th_;
+    std::mutex run_mu_, mu_;
+    std::condition_variable cv_, done_;
+    const std::function<void(unsigned)>* job_ = nullptr;
+    unsigned jobs_ = 0, left_ = 0;
+    uint64_t round_ = 0;
+    bool stop_ = false;
+};
+
+inline WorkerPool& worker_pool() {
+    static WorkerPool pool(host_threads() > 1 ? host_threads() - 1 : 0);
+    return pool;
+}
+
 template <typename F>
 void parallel_docs(size_t n, F&& fn) {
     const unsigned t = (unsigned)std::min<size_t>(host_threads(), std::max<size_t>(1, n / 256));
@@ -308,13 +384,12 @@ void parallel_docs(size_t n, F&& fn) {
         fn(0, n);
         return;
     }
-    std::vector<std::thread> pool;
     const size_t chunk = (n + t - 1) / t;
-    for (unsigned i = 0; i < t; ++i) {
+    const std::function<void(unsigned)> job = [&fn, n, chunk](unsigned i) {
         const size_t lo = i * chunk, hi = std::min(n, lo + chunk);
-        if (lo < hi) pool.emplace_back([&fn, lo, hi] { fn(lo, hi); });
-    }
-    for (auto& th : pool) th.join();
+        if (lo < hi) fn(lo, hi);
+    };
+    worker_pool().run(t, job);
 }
 
 // 64-bit key hash (8-byte words, multiply-xorshift mixing).  Collisions are
@@ -422,22 +497,33 @@ inline bool host_prefetch() {
 // comparison sort.  The destination's ids are its map order, already
 // ascending.  (CRDT_HOST_RANK_IDS=1 instead gives the keys' ranks in string
 // order, the fallback path of the earlier hash-id scheme, kept for tests.)
-struct DocPacker {
-    Batch& b;
-    uint64_t* tk;
-    uint64_t* tc;
-    uint32_t* ta;
-
+// A packing thread's scratch, kept across calls (the worker threads persist).
+struct PackScratch {
     struct Cell {
         uint64_t h;
         const std::string* key;
         uint32_t id, gen;
     };
     std::vector<Cell> cells;
-    uint32_t mask = 0, gen = 0, next = 0;
-    std::vector<Entries::iterator> by_id;  // scratch: a state's element per id (or end)
+    uint32_t gen = 0;
+    std::vector<Entries::iterator> by_id;  // a state's element per id (or end)
     std::vector<uint8_t> has;
     std::vector<const std::string*> sorted;
+};
+
+struct DocPacker {
+    Batch& b;
+    uint64_t* tk;
+    uint64_t* tc;
+    uint32_t* ta;
+    PackScratch& s;
+    using Cell = PackScratch::Cell;
+    std::vector<Cell>& cells = s.cells;
+    uint32_t& gen = s.gen;
+    std::vector<Entries::iterator>& by_id = s.by_id;
+    std::vector<uint8_t>& has = s.has;
+    std::vector<const std::string*>& sorted = s.sorted;
+    uint32_t mask = 0, next = 0;
 
     uint32_t intern(const std::string& k) {
         const uint64_t h = key_hash(k);
@@ -666,7 +752,7 @@ void apply_docs(const Batch& b, size_t n, bool alias, PlanFn&& plan_fn, CommitFn
     if (!alias) {
         const bool pf = host_prefetch();
         parallel_docs(n, [&](size_t lo, size_t hi) {
-            DocPlan p;
+            static thread_local DocPlan p;  // (kept with its thread: its vectors keep their capacity)
             if (pf && lo < hi) prefetch_doc(b, lo);
             for (size_t d = lo; d < hi; ++d) {
                 if (pf && d + 1 < hi) prefetch_doc(b, d + 1);  // one document ahead (2 or 3: no better)
@@ -897,7 +983,8 @@ inline crdt_awset_batch pack(Batch& b, Engine& e, bool tombs) {
     b.sit = e.iters(1, nse);
     t0 = clk::now();
     parallel_docs(n, [&](size_t lo, size_t hi) {
-        DocPacker pk{b, tk, tc, ta, {}, 0, 0, 0, {}, {}, {}};
+        static thread_local PackScratch scratch;
+        DocPacker pk{b, tk, tc, ta, scratch};
         for (size_t d = lo; d < hi; ++d) {
             pk.doc(d);
             const auto& v = b.dst[d]->versionVector;
@@ -1014,8 +1101,19 @@ inline void ExchangeBatch(const std::vector<AWSet*>& as, const std::vector<AWSet
     crdt_awset_out oba = out_arrays(e, kP_OFF, n, b.R, slots);
     oba.keys = oab.keys;  // both directions hold the same keys at the same slots: one column, fetched once
     LastStats().pack_s = secs_since(t0);
+    if (const char* ms = std::getenv("CRDT_HOST_PAUSE_MS"))  // diagnostics: host idle before the device phase
+        std::this_thread::sleep_for(std::chrono::milliseconds(std::atoi(ms)));
     t0 = clk::now();
     check(crdt_awset_exchange_batch(e.ctx(), &ca, &cb, &oab, &oba), "crdt_awset_exchange_batch");
+    if (const char* rep = std::getenv("CRDT_HOST_DEVICE_REPEAT")) {  // diagnostics: the same device call again
+        const double first = secs_since(t0);
+        for (int r = 0; r < std::atoi(rep); ++r) {
+            const auto tr = clk::now();
+            check(crdt_awset_exchange_batch(e.ctx(), &ca, &cb, &oab, &oba), "crdt_awset_exchange_batch");
+            fprintf(stderr, "device call repeat %d: %.3f ms (first %.3f ms)\n", r, secs_since(tr) * 1e3, first * 1e3);
+        }
+        t0 = clk::now() - std::chrono::duration_cast<clk::duration>(std::chrono::duration<double>(first));
+    }
     LastStats().device_s = secs_since(t0);
     t0 = clk::now();
     {

@@ -45,7 +45,9 @@
  * out->counts[d], its slot bounds to out->offsets[d] (n_docs+1 values) and its
  * VV to out->vv.  Entries come out sorted by key.  No scan over documents is
  * needed, so one launch finishes the batch, and the output is directly a valid
- * input batch for the next merge.
+ * input batch for the next merge.  A document's slots past its live count
+ * (counts[d] .. its capacity) are unspecified and may be written (the joins'
+ * whole-sector stores pad them with zeros); slots of other documents never are.
  *
  * Threading: one crdt_ctx per host thread; *_async calls are ordered on the
  * given HIP stream; crdt_ctx_sync returns device-side errors.  Device buffers
@@ -164,20 +166,31 @@ int crdt_ctx_set_max_doc_entries(crdt_ctx* ctx, uint32_t max_entries);
  *                                     blocks (crdt_device.hpp SlabMap; 0 = in order)
  *   "fold_lean_first"     0|1         folds: slot-walk pass first, the rest deferred (default 1)
  *   "join_tile_capacity"  1..2^28     large documents: merge-path tiles of 1,024 merged
- *                                     positions the workspace holds (default 2^22, 56 B
- *                                     each, allocated on first use); a call needing more
- *                                     takes the per-document block kernel instead
+ *                                     positions per pass (default 2^22, 56 B each,
+ *                                     allocated on first use); a call with more tiles runs
+ *                                     in passes of this many, a pass may end inside a
+ *                                     document
+ *   "join_tile_max_passes" 1..65536   passes launched at most (default 256): a call with
+ *                                     more tiles than this x capacity takes the
+ *                                     per-document block kernel instead
  *   "join_tile_dispensers" 1|8        tile dispenser words (default 8, one per XCD)
  *   (also "join_tile_shape", "join_tile_nt_stores", "join_tile_split_blocks_per_cu",
  *   "join_tiles": see api.cpp)
  * and one layout option of the host-buffer (*_batch) joins, exchanges and folds:
  *   "pack_batch_outputs"  0|1         1: out holds only the live entries, doc d
  *                                     at offsets[d] = counts[0] + .. + counts[d-1]
- *                                     (less to download); 0 (default): at its
- *                                     capacity offset, as the *_async calls write.
+ *                                     (less to download; the offsets are computed on the
+ *                                     device, and outputs in crdt_host_alloc memory are
+ *                                     written there by the device, no copy call); 0
+ *                                     (default): at its capacity offset, as the *_async
+ *                                     calls write.
+ *   "span_staging"        0|1         inputs lying in one crdt_host_alloc block go up as
+ *                                     one copy of the span they cover (default 1)
  * The *_batch calls check the slot layout on the host and the key order on the
- * device after the upload (CRDT_E_UNSORTED is then returned after the launch,
- * the outputs unspecified); crdt_validate_batch checks everything on the host. */
+ * device after the upload; a batch out of order reaches no merge kernel (the
+ * merge's first kernel reads the check's verdict on the device) and the call
+ * returns CRDT_E_UNSORTED with the outputs unspecified; crdt_validate_batch
+ * checks everything on the host. */
 int crdt_ctx_set_option(crdt_ctx* ctx, const char* name, int64_t value);
 /* Wait for `stream`, return (and clear) the first device-side error. */
 int crdt_ctx_sync(crdt_ctx* ctx, void* stream);

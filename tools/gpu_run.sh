@@ -27,6 +27,7 @@
 #   ftime    fold timing builds tools/fold_time_$FTIME (space-separated variant names), interleaved, configs 3 and 5
 #   tpass    config-4 exchange in passes of $TCAPS tiles vs one pass (tools/tile_passes.py)
 #   bench1   boundary_bench alone (C++ mirror ExchangeBatch, every document checked)
+#   benv     boundary_bench with per-phase stamps under each runtime setting of $BENV (name:VAR=value pairs)
 set -u
 cd "$(dirname "$0")/.."
 source tools/gpu_step.sh
@@ -136,6 +137,11 @@ for r in "$@"; do
       done ;;
     xab)
       TAILN=12 step xab_$TAG 400 python3 tools/exchange_ab.py ;;
+    benv)
+      for v in ${BENV:-"default:"}; do
+        n=${v%%:*}; e=${v#*:}
+        TAILN=6 step benv_${n}_$TAG 200 env CRDT_TRACE_STAGE=1 $e go-crdt-playground_amd/host/build/boundary_bench 65536
+      done ;;
     tpass)
       TAILN=14 step tpass_$TAG 300 python3 tools/tile_passes.py 16384 ${TCAPS:-4194304 400000 300000} ;;
     bench1)
