@@ -305,14 +305,11 @@ inline unsigned host_threads() {
     return n;
 }
 
-// The worker threads, started once and kept: a thread started and ended per
-// phase allocates through a fresh malloc arena and returns its memory when it
-// ends, and on the GPU box that address-space churn (heap growth and release
-// in the C library's per-thread arenas) made every HIP runtime call of the
-// next device phase block ~1.3 ms (profiles/r06n_boundary_malloc_arenas.log:
-// with at most 4 arenas the device phase of the same call took 6 ms instead of
-// 25).  Kept threads keep their arenas and their scratch (thread_local below),
-// so a steady stream of batch calls allocates almost nothing on the host.
+// The worker threads, started once and kept, with their scratch (thread_local
+// below): a steady stream of batch calls then starts no thread and allocates
+// almost nothing on the host.  Threads started and joined per phase cost the
+// 65,536-document pack ~20 ms (34 -> 13-16 ms with kept threads,
+// profiles/r06n_boundary_malloc_arenas.log vs profiles/r06r_boundary_calls_*.log).
 class WorkerPool {
    public:
     explicit WorkerPool(unsigned n) {
