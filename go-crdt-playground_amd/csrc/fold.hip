@@ -1521,8 +1521,11 @@ __global__ __launch_bounds__(fold_waves<DELTA>() * 64) __attribute__((amdgpu_wav
                 }
             }
             STAMP(10)
-            uint32_t cmax = 0;  // longest source: depth of the re-add search
-            if (DELTA && cur.X) {
+            // (the fused pass searches a source's entries only on a table hit, rare:
+            // it probes every level instead, and the scan below is skipped)
+            constexpr bool kFused = DELTA && LEAN && NCH == 4 && CRDT_FOLD_FUSED;
+            uint32_t cmax = kFused ? 256u : 0u;  // longest source: depth of the re-add search
+            if (DELTA && cur.X && !kFused) {
                 const uint32_t prv = dpp<0x138>(0u, soffv);  // wave_shr:1
                 cmax = lane < ms ? soffv - (lane ? prv : 0u) : 0u;
                 cmax = max(cmax, dpp<0x111>(0u, cmax));  // inclusive max-scan (DPP, no LDS) ...
@@ -1539,7 +1542,6 @@ __global__ __launch_bounds__(fold_waves<DELTA>() * 64) __attribute__((amdgpu_wav
             // The lean delta pass then holds nothing else: a document the fused pass
             // does not take (a full step, a no-op step, > 15 sources, a key span of
             // 256 or more, an actor == len(VV)) is left to the general kernel.
-            constexpr bool kFused = DELTA && LEAN && NCH == 4 && CRDT_FOLD_FUSED;
             if constexpr (kFused) {
                 const int fused =
                     full_mask == 0ull ? fused_delta_walk(m, step, isE, isT, N, n, ms, R, cmax, lane, em, U) : 0;

@@ -27,6 +27,8 @@
 #   ftime    fold timing builds tools/fold_time_$FTIME (space-separated variant names), interleaved, configs 3 and 5
 #   tpass    config-4 exchange in passes of $TCAPS tiles vs one pass (tools/tile_passes.py)
 #   bench1   boundary_bench alone (C++ mirror ExchangeBatch, every document checked)
+#   lab      configs $LCONFIGS (default 3 5) timed by bench.py per library build ($LLIBS: base or X =
+#            tools/libcrdtgpu_X.so), interleaved, three rounds
 #   benv     boundary_bench with per-phase stamps under each runtime setting of $BENV (name:VAR=value pairs)
 set -u
 cd "$(dirname "$0")/.."
@@ -137,6 +139,13 @@ for r in "$@"; do
       done ;;
     xab)
       TAILN=12 step xab_$TAG 400 python3 tools/exchange_ab.py ;;
+    lab)
+      for r in 1 2 3; do for c in ${LCONFIGS:-3 5}; do for v in ${LLIBS:-base}; do
+        lib=go-crdt-playground_amd/crdtgpu/libcrdtgpu.so; [ "$v" = base ] || lib=tools/libcrdtgpu_$v.so
+        TAILN=0 step lab_${v}_c${c}_$r 200 env CRDTGPU_LIB=$PWD/$lib python3 bench.py --config $c --legs none \
+          --steps 50 --warmup 10 --repeats 1 --no-cpu-baseline --no-boundary --no-box-probe --no-sort
+        python3 -c "import json,sys; d=json.loads(open('gpurun_out/lab_${v}_c${c}_$r.log').read().strip().splitlines()[-1]); print('lab $v c$c round $r: %.4f ms frac %.4f' % (d['ms_per_step'], d['roofline']['frac']))" || true
+      done; done; done ;;
     benv)
       for v in ${BENV:-"default:"}; do
         n=${v%%:*}; e=${v#*:}
