@@ -45,8 +45,15 @@ if [ "${EXTRA:-0}" = 1 ]; then
 fi
 cpass calib_fetch FETCH_SIZE
 cpass calib_write WRITE_SIZE
+FP=stream8
+if [ "$CONFIG" = 4 ] && [ -x tools/fetch_calib ]; then  # the tile kernel's element mix, calibrated on its own
+  timeout -k 10 -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/calib_mix" -o run -- tools/fetch_calib \
+    > "$OUT/calib_mix.log" 2>&1
+  mrc=$?; echo "[pmc calib_mix] rc=$mrc"; [ $mrc -eq 0 ] || { tail -20 "$OUT/calib_mix.log"; exit $mrc; }
+  FP=mix
+fi
 # the bench's config-2 exchange shares one key column between its outputs unless BENCH_ARGS has --own-keys
 SK=0
 if [ "$CONFIG" = 2 ]; then case "${BENCH_ARGS:-}" in *--own-keys*) SK=0 ;; *) SK=1 ;; esac; fi
 python3 tools/traffic.py "$OUT" --docs $DOCS --config $CONFIG --kernel "$KERNEL" --tus $TUS --shared-keys $SK \
-  --profile "profiles/${TAG}_pmc_summary.txt" --emit > "$OUT/summary.txt" && cat "$OUT/summary.txt"
+  --profile "profiles/${TAG}_pmc_summary.txt" --fetch-pattern $FP --emit > "$OUT/summary.txt" && cat "$OUT/summary.txt"

@@ -45,6 +45,8 @@ def main():
     ap.add_argument("--shared-keys", type=int, default=0, help="exchange runs: the two outputs shared one key column")
     ap.add_argument("--tus", default="join.hip", help="comma-separated translation units of the kernel (crdtgpu.srcid)")
     ap.add_argument("--profile", default="", help="the profiles/ summary this entry is committed as")
+    ap.add_argument("--fetch-pattern", default="stream8", choices=["stream8", "mix"],
+                    help="FETCH_SIZE correction: 8-byte streaming (calib.py) or the tile element mix (fetch_calib)")
     a = ap.parse_args()
     out, calib = {}, {}
     for sub in sorted(os.listdir(a.dir)):
@@ -64,6 +66,13 @@ def main():
     N = 64 << 20
     fcorr = (16 * N) / (cal["FETCH_SIZE"] * 1024) if cal.get("FETCH_SIZE") else None
     wcorr = (8 * N) / (cal["WRITE_SIZE"] * 1024) if cal.get("WRITE_SIZE") else None
+    # --fetch-pattern mix: the tile kernel's element (u64 key, u32 actor, u64 counter
+    # per lane), calibrated on its own (tools/fetch_calib.hip readmix: 20 B x 64 Mi per launch)
+    mix = calib.get("readmix", {})
+    if a.fetch_pattern == "mix":
+        print("calibration (fetch_calib readmix, 1.25 GiB read per launch):", mix,
+              "read1<u64>:", calib.get("read1<unsigned long long>", {}), "read1<u32>:", calib.get("read1<unsigned int>", {}))
+        fcorr = (20 * N) / (mix["FETCH_SIZE"] * 1024) if mix.get("FETCH_SIZE") else None
     # the exact instance when --kernel names one (has '<'), else the first of the family
     jk = a.kernel if "<" in a.kernel else next((k for k in out if k.startswith(a.kernel)), "")
     j = out.get(jk, {})
@@ -75,7 +84,7 @@ def main():
                                        jk.split(",")[2:3] == [" true"])
     res = {"docs": a.docs, "config": a.config, "kernel": jk, "exchange": exch,
            "src_id": source_id(tuple(x for x in a.tus.split(",") if x)), "profile": a.profile,
-           "fetch_correction": fcorr, "write_correction": wcorr}
+           "fetch_correction": fcorr, "fetch_pattern": a.fetch_pattern, "write_correction": wcorr}
     if res["exchange"]:
         res["shared_keys"] = bool(a.shared_keys)
     if j.get("FETCH_SIZE") is not None and j.get("WRITE_SIZE") is not None:
