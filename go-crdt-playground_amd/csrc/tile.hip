@@ -683,8 +683,8 @@ __global__ __launch_bounds__(NT) void join_tile_kernel(BatchView A, BatchView B,
 // every walk ends (each tile's aggregate is published without waiting, and
 // tile 0 of a document publishes its inclusive count).
 template <int NT, int IPT, bool EXCH, bool NTS, bool ALIGN>
-__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(6))) void join_tile_pipe_kernel(BatchView A, BatchView B, OutView o1, OutView o2,
-                                                            TileWork tw, Work wk) {
+__device__ __forceinline__ void tile_pipe_body(const BatchView& A, const BatchView& B, const OutView& o1,
+                                               const OutView& o2, const TileWork& tw, const Work& wk) {
     __shared__ TileSmem<NT, IPT> sm[2];
     __shared__ uint32_t word[2];
     const uint32_t tid = threadIdx.x, lane = tid & 63;
@@ -778,6 +778,21 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(6))) void jo
     if (__syncthreads_or(err != 0) && tid == 0) atomicOr(wk.status, kErrActorRange);
 }
 
+// Pass 0 of a call, and its later passes under their own name: a call whose
+// tiles the host cannot count (an _async call) launches passes up to a bound,
+// and the later ones usually return at once -- kept apart in kernel traces and
+// counter means, the first pass's figures stay those of the call's tiles.
+template <int NT, int IPT, bool EXCH, bool NTS, bool ALIGN>
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(6))) void join_tile_pipe_kernel(
+    BatchView A, BatchView B, OutView o1, OutView o2, TileWork tw, Work wk) {
+    tile_pipe_body<NT, IPT, EXCH, NTS, ALIGN>(A, B, o1, o2, tw, wk);
+}
+template <int NT, int IPT, bool EXCH, bool NTS, bool ALIGN>
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(6))) void join_tile_pipe_later_kernel(
+    BatchView A, BatchView B, OutView o1, OutView o2, TileWork tw, Work wk) {
+    tile_pipe_body<NT, IPT, EXCH, NTS, ALIGN>(A, B, o1, o2, tw, wk);
+}
+
 // Tile shapes (workgroup size x positions per thread); "join_tile_shape".
 template <int NT, int IPT, bool NTS>
 static hipError_t launch_tile_kernel_s(const BatchView& A, const BatchView& B, const OutView& o1, const OutView* o2,
@@ -814,12 +829,18 @@ static hipError_t launch_tile_pipe_s(const BatchView& A, const BatchView& B, con
         per_cu = nb;
     }
     const dim3 grid(n_cu * per_cu);
-    if (o2)
+    if (tw.pass == 0 && o2)
         hipLaunchKernelGGL((join_tile_pipe_kernel<NT, IPT, true, NTS, ALIGN>), grid, dim3(NT), 0, stream, A, B, o1, *o2, tw,
                            wk);
-    else
+    else if (tw.pass == 0)
         hipLaunchKernelGGL((join_tile_pipe_kernel<NT, IPT, false, NTS, ALIGN>), grid, dim3(NT), 0, stream, A, B, o1, o1, tw,
                            wk);
+    else if (o2)
+        hipLaunchKernelGGL((join_tile_pipe_later_kernel<NT, IPT, true, NTS, ALIGN>), grid, dim3(NT), 0, stream, A, B, o1,
+                           *o2, tw, wk);
+    else
+        hipLaunchKernelGGL((join_tile_pipe_later_kernel<NT, IPT, false, NTS, ALIGN>), grid, dim3(NT), 0, stream, A, B, o1,
+                           o1, tw, wk);
     return hipGetLastError();
 }
 
