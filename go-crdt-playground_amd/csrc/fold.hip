@@ -154,6 +154,9 @@ namespace crdt {
 #endif
 // CRDT_FOLD_FUSED: the lean delta pass's documents with no full step classified
 // and walked in one pass (fused_delta_walk)
+#ifndef CRDT_FOLD_LIST_SPREAD
+#define CRDT_FOLD_LIST_SPREAD 1  // 0: the deferred list in runs of K (A/B builds)
+#endif
 #ifndef CRDT_FOLD_FUSED
 #define CRDT_FOLD_FUSED 1
 #endif
@@ -1124,13 +1127,23 @@ __global__ __launch_bounds__(fold_waves<DELTA>() * 64) __attribute__((amdgpu_wav
     uint32_t err = 0;
     STAMP_DECL
 
-    // LIST: the run is entries [first, first + K) of the deferred list
+    // LIST: the run is entries [first, first + kr) of the deferred list.  Delta
+    // folds: kr = the fewest per wave that cover it (the grid is sized for every
+    // document at K a wave: config 3's list, ~1 % of its documents, is spread one
+    // document a wave over the chip instead of K-long latency chains on ~700
+    // waves -- the call 1.717 -> 1.630 ms, profiles/r06za_lab.log); AWSet folds
+    // keep runs of K (config 5: spread 0.2 % slower)
     const uint32_t n_run = LIST ? min(__hip_atomic_load(wk.defer_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
                                       n_docs)
                                 : n_docs;
-    const uint32_t first = uniform((blockIdx.x * fold_waves<DELTA>() + w) * (uint32_t)K);
+    uint32_t kr = (uint32_t)K;
+    if constexpr (LIST && DELTA && CRDT_FOLD_LIST_SPREAD) {
+        const uint32_t waves = gridDim.x * (uint32_t)fold_waves<DELTA>();
+        kr = uniform(max(1u, min((uint32_t)K, (n_run + waves - 1u) / waves)));
+    }
+    const uint32_t first = uniform((blockIdx.x * fold_waves<DELTA>() + w) * kr);
     if (first >= n_run || !gate_open(wk)) return;  // (a closed gate: nothing deferred or pushed either)
-    const uint32_t cnt = min((uint32_t)K, n_run - first);
+    const uint32_t cnt = min(kr, n_run - first);
 
     // ---- metadata of the run: lane i <= cnt describes document first + i (LIST:
     // lane i < cnt describes deferred document i, with its end bounds loaded)

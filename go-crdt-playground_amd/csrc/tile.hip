@@ -169,7 +169,10 @@ __device__ __forceinline__ uint32_t merge_path_gallop(const uint64_t* dk, const 
 // tile searches only the window its predecessor's split bounds (the split
 // moves by at most one tile along each array: i(t) <= i(t+1) <= i(t) + tile),
 // so the deep levels of the search -- a line fetched per level -- are fewer.
-constexpr uint32_t kSplitRun = 4;
+#ifndef CRDT_TILE_SPLIT_RUN
+#define CRDT_TILE_SPLIT_RUN 4  // (A/B builds)
+#endif
+constexpr uint32_t kSplitRun = CRDT_TILE_SPLIT_RUN;
 
 // Tiles of one pass, plus the first tile of the next pass: its split is where
 // this pass's last tile ends (tile_geo_kernel).
@@ -782,6 +785,10 @@ __device__ __forceinline__ void tile_pipe_body(const BatchView& A, const BatchVi
 // tiles the host cannot count (an _async call) launches passes up to a bound,
 // and the later ones usually return at once -- kept apart in kernel traces and
 // counter means, the first pass's figures stay those of the call's tiles.
+// (waves_per_eu(6) is met by the default shape, 512 x 2; the other shapes' LDS
+// holds them below it, which the compiler reports as a failed occupancy target)
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Wpass-failed"
 template <int NT, int IPT, bool EXCH, bool NTS, bool ALIGN>
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(6))) void join_tile_pipe_kernel(
     BatchView A, BatchView B, OutView o1, OutView o2, TileWork tw, Work wk) {
@@ -792,6 +799,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(6))) void jo
     BatchView A, BatchView B, OutView o1, OutView o2, TileWork tw, Work wk) {
     tile_pipe_body<NT, IPT, EXCH, NTS, ALIGN>(A, B, o1, o2, tw, wk);
 }
+#pragma clang diagnostic pop
 
 // Tile shapes (workgroup size x positions per thread); "join_tile_shape".
 template <int NT, int IPT, bool NTS>
