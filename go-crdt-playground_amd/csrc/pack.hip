@@ -20,16 +20,21 @@ namespace crdt {
 
 constexpr int kPackScanNT = 1024;
 
-// One workgroup: thread t sums a contiguous run of documents, a block scan
-// places the runs, then each thread writes its run's prefixes (poff[n] =
-// total).  host_off (may be NULL): the same offsets, into the caller's
-// page-locked output.
+// One workgroup, in chunks of kPackScanNT x kPackScanV documents: the chunk's
+// live counts are loaded coalesced into LDS, each thread sums kPackScanV
+// consecutive ones, a block scan places the thread runs, the prefixes go back
+// to LDS and out coalesced (poff[n] = total).  Threads reading and writing
+// their own runs straight from memory -- 4-byte accesses 256 bytes apart,
+// through one CU -- took 0.43-0.47 ms for an exchange's 2 x 65,536 documents.
+// host_off (may be NULL): the same offsets, into the caller's page-locked
+// output.
 // gate: the call's status word -- after a failed order check the merge never
 // ran, so the output's slot bounds and counts were never written: every
 // offset is 0 and pack_out_kernel writes nothing.
 // Up to two outputs (an exchange's), one after the other; host_status (may
 // be NULL): the call's status word, copied for the host to read after its sync
 // (the merges that set it have all run; nothing after this kernel sets it).
+constexpr int kPackScanV = 8;
 struct PackScanOut {
     const uint32_t* off;
     const uint32_t* cnt;
@@ -39,37 +44,49 @@ struct PackScanOut {
 __global__ __launch_bounds__(kPackScanNT) void pack_scan_kernel(PackScanOut o0, PackScanOut o1, uint32_t nout,
                                                                 uint32_t n, const uint32_t* gate,
                                                                 uint32_t* host_status) {
+    constexpr uint32_t C = kPackScanNT * kPackScanV;
     __shared__ uint32_t wave_tot[kPackScanNT / 64];
+    __shared__ uint32_t run[C];
     const uint32_t t = threadIdx.x;
     const bool open = (*gate & kErrUnsorted) == 0u;
     if (host_status && t == 0) *host_status = *gate;
     for (uint32_t k = 0; k < nout; ++k) {
-    const PackScanOut& po = k ? o1 : o0;
-    const uint32_t* off = po.off;
-    const uint32_t* cnt = po.cnt;
-    uint32_t* poff = po.poff;
-    uint32_t* host_off = po.host_off;
-    const uint32_t per = (n + kPackScanNT - 1) / kPackScanNT;
-    const uint32_t d0 = min(t * per, n), d1 = min(d0 + per, n);
-    auto live = [&](uint32_t d) -> uint32_t {  // clamped to the capacity (a larger count only follows a failed merge)
-        if (!open) return 0u;
-        const uint32_t c = off[d + 1] - off[d];
-        return min(cnt[d], c);
-    };
-    uint32_t sum = 0;
-    for (uint32_t d = d0; d < d1; ++d) sum += live(d);
-    uint32_t tot = 0;
-    uint32_t p = block_exclusive_scan<kPackScanNT>(sum, wave_tot, &tot);
-    for (uint32_t d = d0; d < d1; ++d) {
-        poff[d] = p;
-        if (host_off) host_off[d] = p;
-        p += live(d);
-    }
-    if (t == 0) {
-        poff[n] = tot;
-        if (host_off) host_off[n] = tot;
-    }
-    __syncthreads();  // (wave_tot is reused by the next output's scan)
+        const PackScanOut& po = k ? o1 : o0;
+        uint32_t carry = 0;
+        for (uint32_t base = 0; base < n; base += C) {
+            const uint32_t m = min(C, n - base);
+            for (uint32_t i = t; i < C; i += kPackScanNT) {
+                const uint32_t d = base + i;
+                // clamped to the capacity (a larger count only follows a failed merge)
+                run[i] = (open && i < m) ? min(po.cnt[d], po.off[d + 1] - po.off[d]) : 0u;
+            }
+            __syncthreads();
+            uint32_t v[kPackScanV], sum = 0;
+#pragma unroll
+            for (int j = 0; j < kPackScanV; ++j) {
+                v[j] = run[t * kPackScanV + j];
+                sum += v[j];
+            }
+            uint32_t tot = 0;
+            uint32_t p = carry + block_exclusive_scan<kPackScanNT>(sum, wave_tot, &tot);
+            // (the scan's barriers order every read of run above before these writes)
+#pragma unroll
+            for (int j = 0; j < kPackScanV; ++j) {
+                run[t * kPackScanV + j] = p;
+                p += v[j];
+            }
+            __syncthreads();
+            for (uint32_t i = t; i < m; i += kPackScanNT) {
+                po.poff[base + i] = run[i];
+                if (po.host_off) po.host_off[base + i] = run[i];
+            }
+            carry += tot;
+            __syncthreads();  // (run and wave_tot are reused by the next chunk)
+        }
+        if (t == 0) {
+            po.poff[n] = carry;
+            if (po.host_off) po.host_off[n] = carry;
+        }
     }
 }
 
