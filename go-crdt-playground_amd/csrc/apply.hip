@@ -335,7 +335,6 @@ __global__ __launch_bounds__(WAVES * 64) void apply_kernel(BatchView st, TombVie
 __global__ __launch_bounds__(256) void tomb_gc_kernel(TombView tb, uint32_t n_docs, uint32_t R, const uint64_t* stable,
                                                       TombOut out) {
     const uint32_t lane = threadIdx.x & 63;
-    const uint64_t lt = low_mask(lane);
     for (uint32_t d = uniform(blockIdx.x * 4 + (threadIdx.x >> 6)); d < n_docs; d += gridDim.x * 4) {
         const uint32_t o = tb.offsets[d], n = live_count(tb.offsets, tb.counts, d);
         const uint64_t* vv = stable + (size_t)d * R;

@@ -30,7 +30,6 @@ __constant__ uint32_t kUnits48[16] = {1, 5, 7, 11, 13, 17, 19, 23, 25, 29, 31, 3
 template <int WAVES>
 __global__ __launch_bounds__(WAVES * 64) void gen_pair_kernel(uint64_t seed, uint32_t n_docs, OutView A, OutView B) {
     const uint32_t lane = threadIdx.x & 63;
-    const uint64_t lt = low_mask(lane);
     for (uint32_t d0 = blockIdx.x * WAVES + (threadIdx.x >> 6); d0 < n_docs; d0 += gridDim.x * WAVES) {
         const uint32_t d = uniform(d0);
         const uint32_t base = d * 64u;
@@ -329,7 +328,6 @@ __device__ __forceinline__ uint64_t zipf_G(uint64_t seed, uint32_t d, uint32_t u
 __global__ __launch_bounds__(256) void gen_zipf_kernel(uint64_t seed, uint32_t n_docs, const uint32_t* offsets,
                                                         OutView A, OutView B) {
     const uint32_t lane = threadIdx.x & 63;
-    const uint64_t lt = low_mask(lane);
     for (uint32_t d0 = blockIdx.x * 4 + (threadIdx.x >> 6); d0 < n_docs; d0 += gridDim.x * 4) {
         const uint32_t d = uniform(d0);
         const uint32_t size = zipf_doc_size(seed, d);
