@@ -408,9 +408,9 @@ class Config3:
     M = 10
     name = "config3"
     kernel = "fold_pipe_kernel"
-    kernel_instance = "fold_pipe_kernel<16, true, true, false>"
+    kernel_instance = "fold_pipe_kernel<8, true, true, false>"
     tus = ("fold.hip",)
-    kernel_name = ("fold_pipe_kernel<16, true, true, false> (per-document fold, delta: lean slot-walk pass, then the "
+    kernel_name = ("fold_pipe_kernel<8, true, true, false> (per-document fold, delta: lean slot-walk pass, then the "
                    "general pass over the documents it defers; timed as the whole call)")
     metric = "replica-merges/sec (AWSetDelta fold, config 3) + achieved HBM GB/s (% roofline)"
     mode = 1  # CRDT_FOLD_DELTA

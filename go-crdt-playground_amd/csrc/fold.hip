@@ -87,7 +87,10 @@ namespace crdt {
 //    97 LDS instructions a document (round 3: 837 / 533 / 104;
 //    profiles/r04c3_pmc_summary.txt);
 //  * documents per wave (CRDT_FOLD_K_DELTA / CRDT_FOLD_K) 8 / 16 and 24 / 48
-//    against 16 / 32: equal or slower on both configs, 16 / 32 kept.
+//    against 16 / 32: equal or slower on both configs, 16 / 32 kept (round 4);
+//    with the fused delta walk (round 6, profiles/r06zj_fold_docs_per_wave.log,
+//    three interleaved rounds each): delta 8 and 6 -1.3-1.9 %, 4 +1.2 %, 12
+//    -0.4 % against 16 -- 8 kept; AWSet 16 / 24 against 32 within noise, 32 kept.
 // 1: survivors staged through LDS and written as contiguous lines -- measured
 // 4 % slower on config 3 and 5 % on config 5 (tools/fold_probe.hip timing
 // builds, three interleaved rounds), so off: each lane stores its own
@@ -1075,7 +1078,7 @@ struct DocMeta {
 #define CRDT_FOLD_K 32
 #endif
 #ifndef CRDT_FOLD_K_DELTA
-#define CRDT_FOLD_K_DELTA 16
+#define CRDT_FOLD_K_DELTA 8
 #endif
 #ifndef CRDT_FOLD_WAVES_DELTA
 #define CRDT_FOLD_WAVES_DELTA 1
@@ -1089,7 +1092,7 @@ constexpr int fold_waves() { return DELTA ? kFoldWavesD : kFoldWaves; }
 // survivors' stores: non-temporal (plain stores measured no faster)
 constexpr int kFoldStoreAux = kAuxNT;
 constexpr int kFoldK = CRDT_FOLD_K;  // consecutive documents per wavefront (AWSet folds)
-constexpr int kFoldKD = CRDT_FOLD_K_DELTA;  // (delta folds: 16, measured 2 % faster than 32 on config 3)
+constexpr int kFoldKD = CRDT_FOLD_K_DELTA;  // (delta folds: 8; 16 was 2 % faster than 32, 8 1.3-1.9 % than 16)
 // stores of one document's write-out: walk rounds x 3 + count + VV
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 // lane E of (hi:lo) := the wave-uniform x (v_writelane: no select, no exec change)

@@ -15,7 +15,7 @@ mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
 case $CONFIG in
   2) KERNEL=${KERNEL:-"join_wave_kernel<4, 8, 2, true, true>"}; TUS=join.hip; DOCS=1048576; STEPS=3 ;;
-  3) KERNEL=${KERNEL:-"fold_pipe_kernel<16, true, true, false>"}; TUS=fold.hip; DOCS=1048576; STEPS=2 ;;
+  3) KERNEL=${KERNEL:-"fold_pipe_kernel<8, true, true, false>"}; TUS=fold.hip; DOCS=1048576; STEPS=2 ;;
   4) KERNEL=${KERNEL:-"join_tile_pipe_kernel<512, 2, true, true, true>"}; TUS=join.hip,tile.hip; DOCS=16384; STEPS=2 ;;
   5) KERNEL=${KERNEL:-"fold_pipe_kernel<32, false, true, false>"}; TUS=fold.hip; DOCS=12500000; STEPS=2 ;;
   *) echo "CONFIG must be 2..5"; exit 2 ;;

@@ -21,7 +21,7 @@ PEAK = 8000.0
 # config -> kernel name prefix of its dominant launch
 KERNELS = {
     "config2": "void crdt::join_wave_kernel<4, 8, 2, true, true>",
-    "config3": "void crdt::fold_pipe_kernel<16, true, true, false>",
+    "config3": "void crdt::fold_pipe_kernel<8, true, true, false>",
     "config4": "void crdt::join_tile_pipe_kernel<512, 2, true, true, true>",
     "config5": "void crdt::fold_pipe_kernel<32, false, true, false>",
 }
