@@ -947,6 +947,29 @@ def test_packed_batch_outputs(torch, what, pinned):
         e.close()
 
 
+@pytest.mark.parametrize("pinned", [False, True], ids=["copied", "pinned"])
+def test_packed_outputs_scan_chunks(torch, pinned):
+    """The packed offsets are scanned in chunks of 8,192 documents (pack.hip,
+    pack_scan_kernel): an exchange of 2 x 8,192 + 37 small documents crosses
+    two chunk carries in each output; offsets and every document bit-exact."""
+    rng = random.Random(8229)
+    R = 2
+    e = crdtgpu.Engine(0)
+    try:
+        e.set_option("pack_batch_outputs", 1)
+        dst, src = join_case(rng, 2 * 8192 + 37, R, lambda: rng.choice([0, 1, 2, 5, 9]), 10 ** 4, 12)
+        g1, g2 = e.exchange(dst, src, pinned=pinned)
+        for got, (rc, want) in ((g1, oracle.join(dst, src)), (g2, oracle.join(src, dst))):
+            assert rc == 0
+            n = dst.n_docs
+            cnt = np.asarray(got.counts[:n]).astype(np.int64)
+            assert (np.asarray(got.offsets[: n + 1]) == np.concatenate([[0], np.cumsum(cnt)])).all()
+            for d in range(0, n, 7):
+                assert out_doc(got, d, R) == out_doc(want, d, R), d
+    finally:
+        e.close()
+
+
 @pytest.mark.parametrize("span", [1, 0], ids=["span", "per_array"])
 @pytest.mark.parametrize("shared", [False, True], ids=["own_keys", "shared_keys"])
 @pytest.mark.parametrize("pinned_out", [False, True], ids=["copied", "pinned"])
