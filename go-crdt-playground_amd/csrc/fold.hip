@@ -160,6 +160,9 @@ namespace crdt {
 #ifndef CRDT_FOLD_LIST_SPREAD
 #define CRDT_FOLD_LIST_SPREAD 1  // 0: the deferred list in runs of K (A/B builds)
 #endif
+#ifndef CRDT_FOLD_XCD_MAP
+#define CRDT_FOLD_XCD_MAP 1  // XCD-contiguous document ranges: 0 none, 1 AWSet lean pass, 2 both lean passes
+#endif
 #ifndef CRDT_FOLD_FUSED
 #define CRDT_FOLD_FUSED 1
 #endif
@@ -1144,7 +1147,19 @@ __global__ __launch_bounds__(fold_waves<DELTA>() * 64) __attribute__((amdgpu_wav
         const uint32_t waves = gridDim.x * (uint32_t)fold_waves<DELTA>();
         kr = uniform(max(1u, min((uint32_t)K, (n_run + waves - 1u) / waves)));
     }
-    const uint32_t first = uniform((blockIdx.x * fold_waves<DELTA>() + w) * kr);
+    // CRDT_FOLD_XCD_MAP: the lean pass's workgroups renumbered so that each XCD
+    // (workgroups are dispatched to the 8 XCDs round-robin) takes one contiguous
+    // range of documents, and neighbouring runs share their edge lines in one
+    // L2.  AWSet lean pass (1, default): config 5 8.52-8.74 ms against 8.55-9.41
+    // for the round-robin order, nine interleaved rounds on two boxes, and far
+    // less spread; the delta pass (2: both) gained nothing on config 3
+    // (profiles/r06zl_fold_xcd_map_ab.log).
+    uint32_t blk = blockIdx.x;
+    if constexpr (LEAN && (CRDT_FOLD_XCD_MAP == 2 || (CRDT_FOLD_XCD_MAP == 1 && !DELTA))) {
+        const uint32_t q = gridDim.x / 8u, r = gridDim.x % 8u, x = blk % 8u;
+        blk = x * q + min(x, r) + blk / 8u;
+    }
+    const uint32_t first = uniform((blk * fold_waves<DELTA>() + w) * kr);
     if (first >= n_run || !gate_open(wk)) return;  // (a closed gate: nothing deferred or pushed either)
     const uint32_t cnt = min(kr, n_run - first);
 
