@@ -25,7 +25,8 @@ merges/s (whole job); roofline: the dominant kernel's algorithmic HBM bytes
 per launch / its mean launch time (HIP events on its stream) against 8 TB/s;
 cpu_baseline: the hash-map C++ restatement of the reference merge
 (oracle/awset_map.cpp) on every host core, with the 1-core figures and the
-sorted-array C oracle beside it.
+sorted-array C oracle beside it; the CPU baselines run after every GPU timing
+(their samples are copied to the host as each config finishes).
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2|3|4|5] [--legs 3,4,5|none]
   torchrun --nproc-per-node N bench.py --gpus N ...   (one process per GPU)
@@ -323,8 +324,9 @@ class Config2:
             rc2, _ = oracle.join(hb, ha)
             assert rc1 == 0 and rc2 == 0
 
-        return _cpu_baselines("first %d docs of the batch, A<-B and B<-A" % n_sample,
-                              lambda th, b: oracle.map_bench_join(ha, hb, True, th, b), run, 2 * n_sample, budget_s)
+        return lambda: _cpu_baselines("first %d docs of the batch, A<-B and B<-A" % n_sample,
+                                      lambda th, b: oracle.map_bench_join(ha, hb, True, th, b), run, 2 * n_sample,
+                                      budget_s)
 
 
 class Config4(Config2):
@@ -396,7 +398,7 @@ class Config4(Config2):
             rc2, _ = oracle.join(hb, ha)
             assert rc1 == 0 and rc2 == 0
 
-        return _cpu_baselines("first %d docs of the batch (%d entries per side), A<-B and B<-A" % (
+        return lambda: _cpu_baselines("first %d docs of the batch (%d entries per side), A<-B and B<-A" % (
             n_sample, int(ha.offsets[-1])), lambda th, b: oracle.map_bench_join(ha, hb, True, th, b), run,
             2 * n_sample, budget_s)
 
@@ -467,14 +469,14 @@ class Config3:
         n_sample = min(self.cpu_docs, self.n)
         hd = _host_batch(self.D, n_sample, self.R)
         hs = _host_srcs(self.S, n_sample, self.R, self.M, 8, 2)
+        mode, merges = self.mode, n_sample * self.M  # (the thunk holds host copies only, not the device batch)
 
         def run():
-            rc, _ = oracle.fold(self.mode, hd, hs)
+            rc, _ = oracle.fold(mode, hd, hs)
             assert rc == 0
 
-        return _cpu_baselines("first %d docs of the batch (%d deltas)" % (n_sample, n_sample * self.M),
-                              lambda th, b: oracle.map_bench_fold(self.mode, hd, hs, th, b), run,
-                              n_sample * self.M, budget_s)
+        return lambda: _cpu_baselines("first %d docs of the batch (%d deltas)" % (n_sample, merges),
+                                      lambda th, b: oracle.map_bench_fold(mode, hd, hs, th, b), run, merges, budget_s)
 
 
 class Config5(Config3):
@@ -530,14 +532,14 @@ class Config5(Config3):
         n_sample = min(self.cpu_docs, self.n)
         hd = _host_batch(self.D, n_sample, self.R)
         hs = _host_srcs(self.S, n_sample, self.R, self.P - 1, self.E, 0)
+        mode, merges = self.mode, n_sample * (self.P - 1)  # (the thunk holds host copies only)
 
         def run():
-            rc, _ = oracle.fold(self.mode, hd, hs)
+            rc, _ = oracle.fold(mode, hd, hs)
             assert rc == 0
 
-        return _cpu_baselines("first %d docs of the batch (%d merges per pass)" % (n_sample, n_sample * (self.P - 1)),
-                              lambda th, b: oracle.map_bench_fold(self.mode, hd, hs, th, b), run,
-                              n_sample * (self.P - 1), budget_s)
+        return lambda: _cpu_baselines("first %d docs of the batch (%d merges per pass)" % (n_sample, merges),
+                                      lambda th, b: oracle.map_bench_fold(mode, hd, hs, th, b), run, merges, budget_s)
 
 
 CONFIGS = {2: Config2, 3: Config3, 4: Config4, 5: Config5}
@@ -731,7 +733,11 @@ def run_config(config, n, args, ctx, steps, warmup, repeats, cpu, box=None):
         res["roofline"]["traffic_gbs"] = traffic / t_launch / 1e9
         res["roofline"]["traffic_frac"] = traffic / t_launch / 1e9 / HBM_PEAK_GBS
     if cpu and rank == 0 and world == 1:
-        res["cpu_baseline"] = W.cpu_baseline(args.cpu_budget)
+        # the host samples are copied now; the CPU work itself runs after every GPU
+        # timing of the bench (main): ~10 s of an idle GPU before a leg lowered its
+        # clocks for the leg's short warmup (configs 3 and 5 3.5 % / 6 % slower,
+        # profiles/r06zp_leg_cpu_baseline_order.log)
+        res["_cpu_baseline"] = W.cpu_baseline(args.cpu_budget)
     del graph, post_graph, W
     torch.cuda.synchronize()
     torch.cuda.empty_cache()
@@ -945,6 +951,11 @@ def main():
                 result["boundary"]["sort_what"] = ("device ingest sort of both replicas of the boundary batch packed "
                                                    "in map iteration order (not on the mirror's path, which places "
                                                    "entries by id directly while packing)")
+    # CPU baselines last, once the GPU timings are done (run_config)
+    for r in [result] + list(result.get("legs", {}).values()):
+        thunk = r.pop("_cpu_baseline", None)
+        if thunk is not None:
+            r["cpu_baseline"] = thunk()
     if rank == 0:
         print(json.dumps(result), flush=True)
     eng.close()
