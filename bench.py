@@ -831,8 +831,8 @@ def main():
     ap.add_argument("--legs", default=None,
                     help="comma-separated configs timed after the headline (default with --config 2: 3,4,5; "
                          "otherwise none); 'none' for the headline only")
-    ap.add_argument("--leg-steps", type=int, default=20)
-    ap.add_argument("--leg-warmup", type=int, default=5)
+    ap.add_argument("--leg-steps", type=int, default=50)
+    ap.add_argument("--leg-warmup", type=int, default=10)
     ap.add_argument("--repeats", type=int, default=3, help="timed runs of the headline (the first is the value)")
     ap.add_argument("--docs", type=int, default=None, help="documents per GPU for the headline")
     ap.add_argument("--seed", type=int, default=0x5EED)
